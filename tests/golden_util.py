@@ -1,0 +1,40 @@
+"""Helpers to read tests/golden/ (fixtures produced by scripts/make_golden.py)."""
+import gzip
+import json
+import os
+
+GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
+
+
+def cases():
+    return sorted(d for d in os.listdir(GOLDEN) if os.path.isfile(os.path.join(GOLDEN, d, "case.json")))
+
+
+def read(case, fname):
+    p = os.path.join(GOLDEN, case, fname)
+    if os.path.exists(p):
+        return open(p, "rb").read()
+    with gzip.open(p + ".gz", "rb") as f:
+        return f.read()
+
+
+def manifest(case):
+    return json.load(open(os.path.join(GOLDEN, case, "case.json")))
+
+
+def materialize(case, d):
+    """Write the case's CLI inputs into directory d; returns (ref, reads, paf) paths."""
+    out = []
+    for fn in ("ref.fa", "reads.fa", "in.paf"):
+        p = os.path.join(d, fn)
+        with open(p, "wb") as f:
+            f.write(read(case, fn))
+        out.append(p)
+    return tuple(out)
+
+
+def runs(case):
+    m = manifest(case)
+    for k, r in enumerate(m["runs"]):
+        exp = {f: read(case, fn) for f, fn in r["files"].items()}
+        yield k, r, exp

@@ -1,0 +1,142 @@
+/*
+ * mpc.h -- C-ABI of libmpc.so, the MI355X (gfx950) pileup + consensus engine.
+ *
+ * Drop-in boundary.  The reference has no FFI: its interface is the CLI of
+ * src/mapped_paf_read_parser.py (:111-121) and three output files (:446-463).
+ * The build keeps that CLI (minion-plasmid-consensus_amd/mapped_paf_read_parser.py)
+ * and moves the work of the reference's Step 4-6 onto the GPU behind this ABI:
+ *
+ *   reference (mapped_paf_read_parser.py)          replaced by
+ *   ---------------------------------------------  -----------------------------
+ *   Step 4 cs tokenizer + processOperation :285-323, :74-104
+ *                                                  mpc_parse()           (K_parse)
+ *   processBaseString_leftIndel/rightIndel :37-72  mpc_index() .. mpc_rows()
+ *                                                  (even-slot layout, tallies)
+ *   Step 5 max depth :332-341                      mpc_consensus()       (K_consensus)
+ *   Step 6 consensus/threshold :348-439            mpc_consensus()       (K_consensus, K_emit)
+ *   whole Step 4-6                                 mpc_run()
+ *
+ * Steps 1-3 (FASTA/PAF ingest, :161-277) and Step 7 (writers) stay on the host.
+ *
+ * Conventions
+ *   - Plain C types only; every buffer is owned by the caller.  The caller
+ *     allocates ONE device workspace of mpc_plan_workspace_bytes() bytes and
+ *     passes it to mpc_plan_bind(); the library never allocates device memory.
+ *   - All device work is enqueued on the caller's stream (hipStream_t passed as
+ *     void*); no call synchronizes the device.
+ *   - Return value: MPC_OK (0) or a negative MPC_E_* code.  Input DATA errors
+ *     (what makes the reference raise and exit 1) are not return codes: they are
+ *     reported in the status words (MPC_BUF_STATUS) after the run, see MPC_DE_*.
+ *   - Threading: one plan per device / stream; plans share no state.
+ */
+#ifndef MPC_H
+#define MPC_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPC_ABI_VERSION 1
+
+/* return codes */
+#define MPC_OK 0
+#define MPC_E_ARG (-1)       /* bad argument or unsupported size (see mpc_last_error) */
+#define MPC_E_HIP (-2)       /* HIP runtime error */
+#define MPC_E_WORKSPACE (-3) /* workspace smaller than mpc_plan_workspace_bytes() */
+#define MPC_E_STATE (-4)     /* phase called out of order / plan not bound */
+
+/* data-error bits in status[MPC_ST_FLAGS]; any bit => the reference exits 1 */
+#define MPC_DE_OP 1u       /* cs does not start with an operator (sys.exit "Unknown operator", :100-102) */
+#define MPC_DE_VALUE 2u    /* int() of a ':' operand fails (ValueError, :77) */
+#define MPC_DE_INDEX 4u    /* write past the reference end / '*' without operand (IndexError) */
+#define MPC_DE_KEY 8u      /* written base not in ACGT (KeyError, :61 / :71) */
+#define MPC_DE_CAPACITY 16u /* row capacity too small: re-plan with status[MPC_ST_ROWS_NEEDED] */
+#define MPC_DE_INTERNAL 32u /* invariant violated (bug) */
+
+/* status words (uint32) at buffer MPC_BUF_STATUS */
+#define MPC_ST_FLAGS 0       /* OR of MPC_DE_* */
+#define MPC_ST_FIRST_READ 1  /* smallest local read index with a data error (0xFFFFFFFF if none) */
+#define MPC_ST_ROWS_NEEDED 2 /* rows (pileup slots incl. empty odd positions) the layout needs */
+#define MPC_ST_MIXED 3       /* downstream (RIGHT) events at gaps that also hold LEFT events */
+#define MPC_ST_WORDS 8
+
+/* Per-read inputs, already in HBM.  One sample = one (assembly, PAF) pair, e.g.
+ * the sense and antisense consensus jobs of Snakefile:401-423 in one launch.
+ * Reads are grouped by sample (sample[] nondecreasing) and, within a sample,
+ * are in the reference's iteration order: first-occurrence order of the PAF
+ * (:237-243, :292). */
+typedef struct {
+  /* ---- device pointers ---- */
+  const uint8_t* ref;      /* concatenated upper-cased references (:163-165) */
+  const int64_t* ref_off;  /* [n_samples+1] offsets into ref */
+  const uint8_t* cs;       /* cs tag text after "cs:" (e.g. "Z::120*ag:7+tt"), concatenated (:231-234) */
+  const int64_t* cs_off;   /* [n_reads+1]; the cs buffer must stay readable up to cs_off[n_reads]+2048 */
+  const int32_t* tstart;   /* [n_reads] PAF column 8, target start (:222) */
+  const uint8_t* up;       /* upstream flanks (read bases before the alignment, :264) */
+  const int64_t* up_off;   /* [n_reads+1] */
+  const uint8_t* down;     /* downstream flanks (:265) */
+  const int64_t* down_off; /* [n_reads+1] */
+  const int32_t* sample;   /* [n_reads] sample id */
+  /* ---- host-side sizes ---- */
+  int32_t n_samples;
+  const int64_t* h_ref_len;    /* host [n_samples] reference lengths n_s (< 2^22) */
+  const int64_t* h_read_begin; /* host [n_samples+1] local reads of sample s: [h_read_begin[s], h_read_begin[s+1]) */
+  int64_t n_reads;             /* local reads */
+  int64_t cs_bytes;            /* cs_off[n_reads] - cs_off[0] */
+  int64_t cs_base;             /* cs_off[0] */
+  /* multi-GPU read sharding (single GPU: 0, n_reads) */
+  int64_t read_offset;         /* global index of local read 0 */
+  int64_t n_reads_global;
+} mpc_input;
+
+typedef struct mpc_plan mpc_plan;
+
+/* named workspace buffers (byte offset + element count via mpc_plan_buffer) */
+enum {
+  MPC_BUF_STATUS = 0,   /* uint32[MPC_ST_WORDS] */
+  MPC_BUF_CALLS,        /* uint32[rows][4]: {base | chrom1<<8 | chrom2<<16, count, count2, total} */
+  MPC_BUF_NCALLS,       /* int32[n_samples+1]: calls of sample s are [ncalls[s], ncalls[s+1]) */
+  MPC_BUF_MAXDEPTH,     /* uint32[n_samples] */
+  MPC_BUF_ROWS,         /* uint32[rows][4]: per-slot A,T,C,G tallies in output order */
+  MPC_BUF_ROWMETA,      /* uint8[rows] bit0 odd position, bit1 first slot of its position */
+  MPC_BUF_RIGHT_KEY,    /* uint32[n_reads_global] mixed downstream keys (multi-GPU exchange) */
+  MPC_BUF_RIGHT_READ,   /* int32[n_reads_global] */
+  MPC_BUF_HASLEFT,      /* uint8[gaps] */
+  MPC_BUF_MAXR,         /* int32[gaps] */
+  MPC_BUF_RUN_M,        /* int32[n_reads_global + gaps] */
+  MPC_BUF_COUNT
+};
+
+int mpc_version(void);
+const char* mpc_last_error(void);
+
+/* Plan for one input shape.  row_cap = capacity of the pileup-row buffers; the
+ * exact need is only known on device after the layout phase (status word
+ * MPC_ST_ROWS_NEEDED) -- if it is exceeded, MPC_DE_CAPACITY is raised and the
+ * caller re-plans with a larger row_cap.  Host-only, no device work. */
+int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** plan);
+int mpc_plan_destroy(mpc_plan* plan);
+int mpc_plan_workspace_bytes(const mpc_plan* plan, size_t* bytes);
+int mpc_plan_bind(mpc_plan* plan, void* workspace, size_t bytes);
+int mpc_plan_buffer(const mpc_plan* plan, int which, size_t* byte_offset, int64_t* count);
+/* update the per-read device pointers (same shape) without re-planning */
+int mpc_plan_set_input(mpc_plan* plan, const mpc_input* in);
+
+/* Phases (single GPU: mpc_run() = all of them).  Between phases a multi-GPU
+ * host inserts the collectives described in DESIGN.md §Multi-GPU. */
+int mpc_parse(mpc_plan* plan, void* stream);        /* cs -> events, i_end, LEFT marks        */
+int mpc_index(mpc_plan* plan, void* stream);        /* downstream keys, stable sort, runs      */
+int mpc_tally(mpc_plan* plan, void* stream);        /* odd tallies, insertion tallies, run M   */
+int mpc_layout(mpc_plan* plan, void* stream);       /* even-slot replay, row offsets           */
+int mpc_rows(mpc_plan* plan, void* stream);         /* depth, row assembly, flank tallies      */
+int mpc_consensus(mpc_plan* plan, double min_depth_factor, double global_threshold_factor,
+                  void* stream);                    /* max depth, calls, compaction            */
+int mpc_run(mpc_plan* plan, double min_depth_factor, double global_threshold_factor, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPC_H */

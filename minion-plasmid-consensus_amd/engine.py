@@ -1,0 +1,270 @@
+"""ctypes binding of libmpc.so (include/mpc.h) + device buffer management.
+
+PyTorch-ROCm is only the allocator/stream provider here: every input and the
+single workspace are torch uint8 tensors on the GPU, and the C-ABI receives
+raw device pointers.  There is no CPU fallback: if libmpc.so or a HIP device
+is missing, :class:`Engine` raises.
+"""
+import ctypes
+import os
+
+import numpy as np
+
+from . import _build
+
+LIB_PATH = _build.LIBMPC
+
+MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED = 0, 1, 2, 3
+DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL = 1, 2, 4, 8, 16, 32
+(BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_KEY, BUF_RIGHT_READ,
+ BUF_HASLEFT, BUF_MAXR, BUF_RUN_M) = range(11)
+
+DE_NAMES = {DE_OP: "Unknown operator", DE_VALUE: "ValueError", DE_INDEX: "IndexError", DE_KEY: "KeyError",
+            DE_CAPACITY: "row capacity", DE_INTERNAL: "internal invariant"}
+CS_PAD = 2048  # readable bytes required past the end of the cs buffer (mpc.h)
+
+
+class MpcError(RuntimeError):
+    pass
+
+
+class DataError(Exception):
+    """Input the reference rejects (exit status 1).  ``flags`` are MPC_DE_* bits."""
+
+    def __init__(self, flags, read):
+        names = [v for k, v in DE_NAMES.items() if flags & k]
+        super().__init__(f"{'/'.join(names)} (first offending read index {read})")
+        self.flags = flags
+        self.read = read
+
+
+class _Input(ctypes.Structure):
+    _fields_ = [
+        ("ref", ctypes.c_void_p), ("ref_off", ctypes.c_void_p),
+        ("cs", ctypes.c_void_p), ("cs_off", ctypes.c_void_p),
+        ("tstart", ctypes.c_void_p),
+        ("up", ctypes.c_void_p), ("up_off", ctypes.c_void_p),
+        ("down", ctypes.c_void_p), ("down_off", ctypes.c_void_p),
+        ("sample", ctypes.c_void_p),
+        ("n_samples", ctypes.c_int32),
+        ("h_ref_len", ctypes.POINTER(ctypes.c_int64)),
+        ("h_read_begin", ctypes.POINTER(ctypes.c_int64)),
+        ("n_reads", ctypes.c_int64),
+        ("cs_bytes", ctypes.c_int64),
+        ("cs_base", ctypes.c_int64),
+        ("read_offset", ctypes.c_int64),
+        ("n_reads_global", ctypes.c_int64),
+    ]
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise MpcError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() (no CPU fallback)")
+        L = ctypes.CDLL(LIB_PATH)
+        vp, i64, i32, dbl = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double
+        L.mpc_version.restype = i32
+        L.mpc_last_error.restype = ctypes.c_char_p
+        L.mpc_plan_create.argtypes = [ctypes.POINTER(_Input), i64, ctypes.POINTER(vp)]
+        L.mpc_plan_destroy.argtypes = [vp]
+        L.mpc_plan_workspace_bytes.argtypes = [vp, ctypes.POINTER(ctypes.c_size_t)]
+        L.mpc_plan_bind.argtypes = [vp, vp, ctypes.c_size_t]
+        L.mpc_plan_buffer.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(i64)]
+        L.mpc_plan_set_input.argtypes = [vp, ctypes.POINTER(_Input)]
+        for f in ("mpc_parse", "mpc_index", "mpc_tally", "mpc_layout", "mpc_rows"):
+            getattr(L, f).argtypes = [vp, vp]
+        L.mpc_consensus.argtypes = [vp, dbl, dbl, vp]
+        L.mpc_run.argtypes = [vp, dbl, dbl, vp]
+        for f in ("mpc_plan_create", "mpc_plan_destroy", "mpc_plan_workspace_bytes", "mpc_plan_bind",
+                  "mpc_plan_buffer", "mpc_plan_set_input", "mpc_parse", "mpc_index", "mpc_tally",
+                  "mpc_layout", "mpc_rows", "mpc_consensus", "mpc_run"):
+            getattr(L, f).restype = i32
+        _lib = L
+    return _lib
+
+
+def _check(rc):
+    if rc != 0:
+        raise MpcError(f"libmpc error {rc}: {lib().mpc_last_error().decode(errors='replace')}")
+
+
+def _torch():
+    import torch
+    return torch
+
+
+class Batch:
+    """Device-resident inputs of one launch: one or more samples (strands /
+    plasmids) concatenated, reads grouped by sample."""
+
+    def __init__(self, samples, device=0, read_offset=0, n_reads_global=None):
+        torch = _torch()
+        if not torch.cuda.is_available():
+            raise MpcError("no HIP device visible (the pileup path has no CPU fallback)")
+        self.device = torch.device("cuda", device)
+        S = len(samples)
+        self.n_samples = S
+        self.ref_len = np.array([len(s["ref"]) for s in samples], dtype=np.int64)
+        counts = np.array([len(s["tstart"]) for s in samples], dtype=np.int64)
+        self.read_begin = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
+        self.n_reads = int(self.read_begin[-1])
+        self.read_offset = int(read_offset)
+        self.n_reads_global = int(n_reads_global if n_reads_global is not None else self.n_reads)
+
+        def cat_bytes(key, offkey):
+            bufs, offs, base = [], [], 0
+            for s in samples:
+                b = np.asarray(s[key], dtype=np.uint8)
+                o = np.asarray(s[offkey], dtype=np.int64)
+                bufs.append(b[o[0]:o[-1]] if len(o) else b[:0])
+                offs.append((o[:-1] - o[0] + base) if len(o) else o)
+                base += (o[-1] - o[0]) if len(o) else 0
+            data = np.concatenate(bufs) if bufs else np.zeros(0, np.uint8)
+            off = np.concatenate(offs + [np.array([base], dtype=np.int64)])
+            return data, off
+
+        cs, cs_off = cat_bytes("cs", "cs_off")
+        up, up_off = cat_bytes("up", "up_off")
+        dn, dn_off = cat_bytes("down", "down_off")
+        refs = [np.asarray(s["ref"], dtype=np.uint8) for s in samples]
+        ref = np.concatenate(refs) if refs else np.zeros(0, np.uint8)
+        ref_off = np.concatenate([[0], np.cumsum([len(r) for r in refs])]).astype(np.int64)
+        tstart = np.concatenate([np.asarray(s["tstart"], dtype=np.int64) for s in samples])
+        if len(tstart) and (tstart.min() < -(2 ** 31) or tstart.max() >= 2 ** 31):
+            raise MpcError("target start out of int32 range")
+        sample = np.repeat(np.arange(S, dtype=np.int32), counts)
+        self.cs_bytes = int(cs_off[-1])
+        self.aligned_bases = int(sum(int(np.asarray(s.get("aligned", [0])).sum()) for s in samples))
+
+        def dev(a, pad=0):
+            a = np.ascontiguousarray(a)
+            t = torch.empty(max(a.nbytes + pad, 16), dtype=torch.uint8, device=self.device)
+            if a.nbytes:
+                t[: a.nbytes].copy_(torch.from_numpy(a.view(np.uint8).reshape(-1)))
+            if pad:
+                t[a.nbytes:].zero_()
+            return t
+
+        self.t = dict(
+            ref=dev(ref), ref_off=dev(ref_off), cs=dev(cs, CS_PAD), cs_off=dev(cs_off),
+            tstart=dev(tstart.astype(np.int32)), up=dev(up), up_off=dev(up_off),
+            down=dev(dn), down_off=dev(dn_off), sample=dev(sample),
+        )
+        self.h_cs_off = cs_off
+        self.max_flank = int(max((np.diff(up_off).max() if len(up_off) > 1 else 0),
+                                 (np.diff(dn_off).max() if len(dn_off) > 1 else 0)))
+
+    def c_input(self):
+        t = self.t
+        self._keep = (np.ascontiguousarray(self.ref_len), np.ascontiguousarray(self.read_begin))
+        return _Input(
+            ref=t["ref"].data_ptr(), ref_off=t["ref_off"].data_ptr(), cs=t["cs"].data_ptr(),
+            cs_off=t["cs_off"].data_ptr(), tstart=t["tstart"].data_ptr(), up=t["up"].data_ptr(),
+            up_off=t["up_off"].data_ptr(), down=t["down"].data_ptr(), down_off=t["down_off"].data_ptr(),
+            sample=t["sample"].data_ptr(), n_samples=self.n_samples,
+            h_ref_len=self._keep[0].ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+            h_read_begin=self._keep[1].ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+            n_reads=self.n_reads, cs_bytes=self.cs_bytes, cs_base=0,
+            read_offset=self.read_offset, n_reads_global=self.n_reads_global,
+        )
+
+    def row_estimate(self):
+        n = self.ref_len
+        return int((4 * n + 8).sum() + 4 * self.max_flank * self.n_samples + 1024)
+
+
+class Plan:
+    """A bound plan: one workspace for one Batch shape."""
+
+    def __init__(self, batch, row_cap=None):
+        torch = _torch()
+        self.batch = batch
+        self.row_cap = int(row_cap or batch.row_estimate())
+        L = lib()
+        self._inp = batch.c_input()
+        h = ctypes.c_void_p()
+        _check(L.mpc_plan_create(ctypes.byref(self._inp), self.row_cap, ctypes.byref(h)))
+        self.h = h
+        nb = ctypes.c_size_t()
+        _check(L.mpc_plan_workspace_bytes(h, ctypes.byref(nb)))
+        self.ws_bytes = nb.value
+        self.ws_raw = torch.empty(self.ws_bytes + 256, dtype=torch.uint8, device=batch.device)
+        pad = (-self.ws_raw.data_ptr()) % 256
+        self.ws = self.ws_raw[pad: pad + self.ws_bytes]
+        _check(L.mpc_plan_bind(h, ctypes.c_void_p(self.ws.data_ptr()), self.ws_bytes))
+
+    def __del__(self):
+        h = getattr(self, "h", None)
+        if h is not None and _lib is not None:
+            _lib.mpc_plan_destroy(h)
+            self.h = None
+
+    def buffer(self, which, dtype):
+        torch = _torch()
+        off, cnt = ctypes.c_size_t(), ctypes.c_int64()
+        _check(lib().mpc_plan_buffer(self.h, which, ctypes.byref(off), ctypes.byref(cnt)))
+        item = torch.empty(0, dtype=dtype).element_size()
+        return self.ws[off.value: off.value + cnt.value * item].view(dtype)
+
+    def stream_ptr(self, stream=None):
+        torch = _torch()
+        s = stream if stream is not None else torch.cuda.current_stream(self.batch.device)
+        return ctypes.c_void_p(s.cuda_stream)
+
+    def run(self, mdf, gtf, stream=None):
+        _check(lib().mpc_run(self.h, float(mdf), float(gtf), self.stream_ptr(stream)))
+
+    def phase(self, name, stream=None, *args):
+        fn = getattr(lib(), "mpc_" + name)
+        if name == "consensus":
+            _check(fn(self.h, float(args[0]), float(args[1]), self.stream_ptr(stream)))
+        else:
+            _check(fn(self.h, self.stream_ptr(stream)))
+
+    def status(self):
+        torch = _torch()
+        return self.buffer(BUF_STATUS, torch.int32).cpu().numpy().view(np.uint32)
+
+    def fetch(self):
+        """Copy the calls of every sample to the host.  Raises DataError when
+        the reference would have failed on this input."""
+        torch = _torch()
+        st = self.status()
+        flags = int(st[MPC_ST_FLAGS])
+        if flags:
+            raise DataError(flags, int(st[MPC_ST_FIRST_READ]))
+        nc = self.buffer(BUF_NCALLS, torch.int32).cpu().numpy()
+        total = int(nc[-1])
+        calls = self.buffer(BUF_CALLS, torch.int32)[: total * 4].cpu().numpy().view(np.uint32).reshape(-1, 4)
+        md = self.buffer(BUF_MAXDEPTH, torch.int32).cpu().numpy().view(np.uint32)
+        out = []
+        for s in range(self.batch.n_samples):
+            c = calls[nc[s]: nc[s + 1]]
+            out.append(dict(
+                base=(c[:, 0] & 0xFF).astype(np.uint8), chrom1=((c[:, 0] >> 8) & 0xFF).astype(np.uint8),
+                chrom2=((c[:, 0] >> 16) & 0xFF).astype(np.uint8), count=c[:, 1].astype(np.int64),
+                count2=c[:, 2].astype(np.int64), total=c[:, 3].astype(np.int64), max_depth=int(md[s]),
+            ))
+        return out
+
+
+def pileup(samples, mdf, gtf, device=0, row_cap=None):
+    """One-shot helper: samples (packed dicts) -> per-sample call dicts.
+    Re-plans once if the row capacity estimate was too small."""
+    torch = _torch()
+    batch = Batch(samples, device=device)
+    plan = Plan(batch, row_cap)
+    plan.run(mdf, gtf)
+    st = plan.status()
+    flags = int(st[MPC_ST_FLAGS])
+    if flags & DE_CAPACITY and not (flags & ~DE_CAPACITY):
+        need = int(st[MPC_ST_ROWS_NEEDED])
+        plan = Plan(batch, need + 16)
+        plan.run(mdf, gtf)
+    res = plan.fetch()
+    torch.cuda.synchronize(batch.device)
+    return res

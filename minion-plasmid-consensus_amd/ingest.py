@@ -1,0 +1,149 @@
+"""Host ingest: Steps 1-3 of /root/reference/src/mapped_paf_read_parser.py.
+
+Produces the packed per-read arrays the device path consumes.  The semantics
+follow the reference line by line (text mode with universal newlines, str
+rstrip/upper/split, Python int(), first alignment per read name wins, whole
+header line as the read name, Python slicing for the flanks); where the
+reference raises, this raises :class:`IngestError` (the CLI then exits 1 and
+writes nothing, like the reference).
+
+  Step 1  reference FASTA       :161-184  -> read_reference()
+  Step 2  PAF                   :192-245  -> read_paf()
+  Step 3  reads FASTA + flanks  :253-277  -> read_flanks()
+"""
+import numpy as np
+
+BASE_COMPLIMENT = {"A": "T", "T": "A", "G": "C", "C": "G", "N": "N"}  # :27
+_RC_TABLE = str.maketrans("ACGTN", "TGCAN")
+_ALLOWED_RC = frozenset("ACGTN")
+
+
+class IngestError(Exception):
+    """An input the reference rejects (it would raise and exit with status 1)."""
+
+
+def read_reference(path):
+    """Concatenate every non-header line, rstrip()ed and upper-cased (:161-165)."""
+    parts = []
+    with open(path, "r") as fh:
+        for line in fh:
+            if not line.startswith(">"):
+                parts.append(line.rstrip().upper())
+    return "".join(parts)
+
+
+def read_paf(path):
+    """First alignment per read name (:237-243), in first-occurrence order.
+
+    Returns (records, n_lines); each record is [name, qs', qe', tstart, strand, cs].
+    """
+    recs = {}
+    n_lines = 0
+    with open(path, "r") as fh:
+        for line in fh:
+            f = line.rstrip().split("\t")
+            n_lines += 1
+            try:
+                name = f[0]
+                qlen = int(f[1])
+                qs = int(f[2])
+                qe = int(f[3])
+                ts = int(f[7])
+                strand = f[4]
+            except (IndexError, ValueError) as e:
+                raise IngestError(f"PAF line {n_lines}: {type(e).__name__}: {e}") from None
+            if strand == "-":
+                qs, qe = qlen - qe, qlen - int(f[2])  # :226-228
+            cs = None
+            for e in f:  # first field starting with "cs:" (:231)
+                if e.startswith("cs:"):
+                    cs = e[3:]
+                    break
+            if cs is None:
+                raise IngestError(f"PAF line {n_lines}: IndexError: no cs: tag")
+            if name not in recs:
+                recs[name] = [name, qs, qe, ts, strand, cs]
+    return list(recs.values()), n_lines
+
+
+def read_flanks(path, recs):
+    """Upstream / downstream flanks of every PAF read (:253-277).
+
+    Only records named in the PAF are materialized: for the others the
+    reference only runs rstrip()/upper(), which cannot fail.  A duplicate FASTA
+    name is processed again and the last one wins.
+    """
+    by_name = {r[0]: r for r in recs}
+    flanks = {}
+    name = ""
+    seq_parts = None
+
+    def finish(name, parts):
+        r = by_name.get(name)
+        if name == "" or r is None:
+            return
+        seq = "".join(parts)
+        if r[4] == "-":
+            bad = set(seq) - _ALLOWED_RC
+            if bad:
+                raise IngestError(f"KeyError: {sorted(bad)[0]!r} (reverse complement of read {name})")
+            seq = seq[::-1].translate(_RC_TABLE)
+        flanks[name] = (seq[: r[1]], seq[r[2]:])
+
+    with open(path, "r") as fh:
+        for line in fh:
+            if line.startswith(">"):
+                if seq_parts is not None:
+                    finish(name, seq_parts)
+                name = line.rstrip()[1:]
+                seq_parts = [] if name in by_name else None
+            elif seq_parts is not None:
+                seq_parts.append(line.rstrip().upper())
+    if seq_parts is not None:
+        finish(name, seq_parts)
+    return flanks
+
+
+def _ascii(s, what):
+    try:
+        return s.encode("ascii")
+    except UnicodeEncodeError:
+        raise IngestError(f"non-ASCII character in {what} (unsupported)") from None
+
+
+def _concat(items):
+    off = np.zeros(len(items) + 1, dtype=np.int64)
+    if items:
+        np.cumsum(np.fromiter((len(x) for x in items), dtype=np.int64, count=len(items)), out=off[1:])
+    return b"".join(items), off
+
+
+def pack_sample(ref_path, paf_path, reads_path):
+    """Steps 1-3 for one (assembly, PAF) sample -> dict of packed numpy arrays."""
+    refseq = read_reference(ref_path)
+    recs, n_lines = read_paf(paf_path)
+    flanks = read_flanks(reads_path, recs)
+    cs, up, down, ts, aligned = [], [], [], [], []
+    for name, qs, qe, t, strand, c in recs:
+        fl = flanks.get(name)
+        if fl is None:  # paf[read_name]["upstream_seq"] -> KeyError (:303)
+            raise IngestError(f"KeyError: 'upstream_seq' (read {name} not in {reads_path})")
+        if t < 0 or t >= 2 ** 31:
+            raise IngestError(f"target start {t} of read {name} out of range (unsupported)")
+        cs.append(_ascii(c, "cs tag"))
+        up.append(_ascii(fl[0], "read sequence"))
+        down.append(_ascii(fl[1], "read sequence"))
+        ts.append(t)
+        aligned.append(qe - qs)
+    cs_b, cs_off = _concat(cs)
+    up_b, up_off = _concat(up)
+    dn_b, dn_off = _concat(down)
+    return dict(
+        ref=np.frombuffer(_ascii(refseq, "reference"), dtype=np.uint8),
+        cs=np.frombuffer(cs_b, dtype=np.uint8), cs_off=cs_off,
+        tstart=np.asarray(ts, dtype=np.int64),
+        up=np.frombuffer(up_b, dtype=np.uint8), up_off=up_off,
+        down=np.frombuffer(dn_b, dtype=np.uint8), down_off=dn_off,
+        aligned=np.asarray(aligned, dtype=np.int64),
+        n_alignments=n_lines,
+    )

@@ -1,0 +1,92 @@
+"""Drop-in CLI for src/mapped_paf_read_parser.py (reference v5.1, :108-465).
+
+Same flags, same output files, same exit status; Steps 4-6 run on an MI355X
+through libmpc.so.  The Snakemake rule `consensus` (Snakefile:401-423) only has
+to point ``params.script`` here.
+
+Extra, optional flags (defaults keep the reference behaviour):
+  --device N         HIP device index (default 0)
+  --also REF PAF CONSENSUS CHROMAT ACCURACIES
+                     run another (assembly, PAF) pair against the same --reads in
+                     the SAME launch (e.g. the antisense strand); repeatable
+"""
+import argparse
+import importlib
+import os
+import sys
+import time
+
+TITLE = "Mapped PAF Read Parser"
+
+
+def statprint(msg, msg_type="STATUS"):
+    print("{} [{}]: {}".format(msg_type, time.strftime("%Y/%m/%d %T"), msg), flush=True)
+
+
+def _pkg():
+    if __package__:
+        return importlib.import_module(__package__)
+    here = os.path.dirname(os.path.abspath(__file__))
+    sys.path.insert(0, os.path.dirname(here))
+    return importlib.import_module(os.path.basename(here))
+
+
+def build_parser():
+    p = argparse.ArgumentParser(description=TITLE)
+    p.add_argument("--ref", dest="REF", help="Reference fasta file of plasmid sequence", type=str)
+    p.add_argument("--reads", dest="READS", help="Raw reads fasta file", type=str)
+    p.add_argument("--paf", dest="PAF", help="Mapped reads .paf file", type=str)
+    p.add_argument("--consensus", help="Consensus output file", type=str)
+    p.add_argument("--chromat", help="Chromatogram data output file", type=str)
+    p.add_argument("--accuracies", help="Per position consensus accuracies output file", type=str)
+    p.add_argument("--min_depth_factor", dest="MIN_DEPTH_FACTOR", type=float,
+                   help="Minimum number of reads needed to call a base is set to max_depth*MIN_DEPTH_FACTOR")
+    p.add_argument("--global_threshold_factor", dest="GLOBAL_THRESHOLD_FACTOR", type=float,
+                   help="Value of minimum most frequent to second most frequent base ratio to make call")
+    p.add_argument("-d", "--debug", action="store_true", dest="DEBUG", help="Flag for setting debug/test state.")
+    p.add_argument("-v", "--verbose", action="store_true", dest="VERB", help="Flag for setting verbose output.")
+    p.add_argument("--device", type=int, default=0, help="HIP device index")
+    p.add_argument("--also", nargs=5, action="append", default=[],
+                   metavar=("REF", "PAF", "CONSENSUS", "CHROMAT", "ACCURACIES"),
+                   help="additional (assembly, PAF) job against the same reads, same launch")
+    return p
+
+
+def main(argv=None):
+    args = build_parser().parse_args(argv)
+    pkg = _pkg()
+    ingest, engine, writers = pkg.ingest, pkg.engine, pkg.writers
+    print("=======================================================")
+    print("Python version: {}".format(sys.version))
+    print("Command: {}".format(" ".join(sys.argv)))
+    print("Time: {}".format(time.strftime("%Y/%m/%d %T")))
+    print("Engine: libmpc (HIP, gfx950)")
+    print("=======================================================\n")
+    jobs = [(args.REF, args.PAF, args.consensus, args.chromat, args.accuracies)] + [tuple(a) for a in args.also]
+    try:
+        samples = []
+        for ref, paf, *_ in jobs:
+            statprint(f"Ingesting {paf} against {ref}...")
+            samples.append(ingest.pack_sample(ref, paf, args.READS))
+            statprint("There were {} mapped reads.".format(samples[-1]["n_alignments"]))
+        if args.MIN_DEPTH_FACTOR is None:
+            raise ingest.IngestError("TypeError: --min_depth_factor is required")  # max_depth*None (:338)
+        gtf = args.GLOBAL_THRESHOLD_FACTOR
+        statprint("Pileup and consensus on device {}...".format(args.device))
+        results = engine.pileup(samples, args.MIN_DEPTH_FACTOR, 1.0 if gtf is None else gtf, device=args.device)
+        if gtf is None and any(len(r["count"]) or r["max_depth"] for r in results):
+            raise ingest.IngestError("TypeError: --global_threshold_factor is required")  # (:421)
+    except (ingest.IngestError, engine.DataError, OSError) as e:
+        print("Error: {}".format(e), file=sys.stderr)
+        return 1
+    for (ref, paf, c, ch, acc), res in zip(jobs, results):
+        statprint("Max depth is {}.".format(res["max_depth"]))
+        statprint("DEPTH_THRESHOLD is {}.".format(res["max_depth"] * args.MIN_DEPTH_FACTOR))
+        statprint("Writing consensus, chromatogram data and per-position consensus accuracies...")
+        writers.write_outputs(res, c, ch, acc)
+    statprint("Done.")
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

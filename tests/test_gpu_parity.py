@@ -1,0 +1,113 @@
+"""Parity of the HIP path (through the C-ABI) with the reference and the oracle.
+
+  * every golden case (outputs of the reference script itself) through the
+    drop-in CLI: identical bytes in all three files and identical exit status
+  * seeded synthetic batches vs the C oracle, call by call, with
+    min_depth_factor = -1 (every pileup slot is emitted: full-pileup parity)
+"""
+import importlib
+import os
+
+import numpy as np
+import pytest
+
+import golden_util as gu
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+KEYS = ("base", "chrom1", "chrom2", "count", "count2", "total")
+
+
+@pytest.fixture(scope="module")
+def cli():
+    return importlib.import_module("minion-plasmid-consensus_amd.mapped_paf_read_parser")
+
+
+@pytest.mark.parametrize("case", gu.cases())
+def test_cli_matches_reference(case, tmp_path, cli):
+    ref, reads, paf = gu.materialize(case, str(tmp_path))
+    for k, run, exp in gu.runs(case):
+        outs = [str(tmp_path / f"o{k}_{x}") for x in ("c.fa", "ch.tsv", "acc.tsv")]
+        rc = cli.main(["--ref", ref, "--reads", reads, "--paf", paf, "--consensus", outs[0], "--chromat", outs[1],
+                       "--accuracies", outs[2], "--min_depth_factor", repr(run["mdf"]),
+                       "--global_threshold_factor", repr(run["gtf"])])
+        assert rc == run["exit"], (case, k)
+        if rc == 0:
+            for o, f in zip(outs, ("c.fa", "ch.tsv", "acc.tsv")):
+                assert open(o, "rb").read() == exp[f], (case, k, f)
+        else:
+            assert not any(os.path.exists(o) for o in outs), "no partial outputs on failure"
+
+
+def _oracle(s, mdf, gtf):
+    return oracle.run_packed(s["ref"], s["cs"], s["cs_off"], s["tstart"], s["up"], s["up_off"], s["down"],
+                             s["down_off"], mdf, gtf)
+
+
+def _cmp(got, exp, tag):
+    assert got["max_depth"] == exp["max_depth"], tag
+    for k in KEYS:
+        a = np.asarray(got[k], dtype=np.int64)
+        b = np.asarray(exp[k], dtype=np.int64)
+        assert a.shape == b.shape, (tag, k, a.shape, b.shape)
+        if not np.array_equal(a, b):
+            bad = np.nonzero(a != b)[0][:5]
+            raise AssertionError(f"{tag} {k} differs at {bad.tolist()}: {a[bad].tolist()} vs {b[bad].tolist()}")
+
+
+SYNTH = [
+    dict(n=2686, n_reads=3000, profile="default", seed=2, frac_partial=0.02),
+    dict(n=1500, n_reads=2000, profile="default", seed=21, frac_partial=0.4),
+    dict(n=1000, n_reads=1500, profile="indel", seed=4, frac_partial=0.1),
+    dict(n=700, n_reads=800, profile="indel", seed=41, frac_partial=0.6, ins_len=(1, 12), del_len=(1, 30),
+         flank=(0, 200)),
+    dict(n=50, n_reads=2000, profile="c1probe", seed=7, frac_partial=0.5, flank=(0, 8)),
+    dict(n=3000, n_reads=500, profile="default", seed=9, frac_partial=0.3, ins_len=(1, 1500), del_len=(1, 1200),
+         p_ins=0.0005, p_del=0.0005, flank=(0, 3000)),
+]
+
+
+@pytest.mark.parametrize("spec", SYNTH, ids=lambda s: f"n{s['n']}_N{s['n_reads']}_{s['profile']}_s{s['seed']}")
+def test_synthetic_full_pileup(pkg, spec):
+    syn = pkg.synth.Synth(**spec)
+    samples = [syn.sample(0), syn.sample(1)]
+    for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0), (0.5, 2.5)):
+        res = pkg.engine.pileup(samples, mdf, gtf)
+        for s, (smp, r) in enumerate(zip(samples, res)):
+            _cmp(r, _oracle(smp, mdf, gtf), (spec["seed"], s, mdf, gtf))
+
+
+def test_repeat_launches_identical(pkg):
+    """Integer atomics: the result does not depend on wave scheduling."""
+    syn = pkg.synth.Synth(n=1200, n_reads=4000, profile="indel", seed=77, frac_partial=0.3)
+    samples = [syn.sample(0)]
+    batch = pkg.engine.Batch(samples)
+    plan = pkg.engine.Plan(batch, row_cap=200000)
+    first = None
+    for _ in range(5):
+        plan.run(-1.0, 1.0)
+        got = plan.fetch()[0]
+        if first is None:
+            first = got
+            _cmp(got, _oracle(samples[0], -1.0, 1.0), "repeat")
+        else:
+            _cmp(got, first, "repeat")
+
+
+def test_capacity_replan(pkg):
+    syn = pkg.synth.Synth(n=400, n_reads=500, profile="default", seed=3, frac_partial=0.5, flank=(0, 100))
+    samples = [syn.sample(0)]
+    res = pkg.engine.pileup(samples, -1.0, 1.0, row_cap=10)
+    _cmp(res[0], _oracle(samples[0], -1.0, 1.0), "replan")
+
+
+def test_many_samples_one_launch(pkg):
+    samples, exp = [], []
+    for k in range(12):
+        syn = pkg.synth.Synth(n=300 + 37 * k, n_reads=200 + 20 * k, profile="indel" if k % 2 else "default",
+                              seed=100 + k, frac_partial=0.2, antisense=False)
+        samples.append(syn.sample(0))
+    res = pkg.engine.pileup(samples, 0.1, 5.0)
+    for k, (s, r) in enumerate(zip(samples, res)):
+        _cmp(r, _oracle(s, 0.1, 5.0), ("multi", k))

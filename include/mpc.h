@@ -75,7 +75,8 @@ typedef struct {
   const uint8_t* cs;       /* cs tag text after "cs:" (e.g. "Z::120*ag:7+tt"), concatenated (:231-234) */
   const int64_t* cs_off;   /* [n_reads+1]; the cs buffer must stay readable up to cs_off[n_reads]+2048 */
   const int32_t* tstart;   /* [n_reads] PAF column 8, target start (:222) */
-  const uint8_t* up;       /* upstream flanks (read bases before the alignment, :264) */
+  const uint8_t* up;       /* upstream flanks (read bases before the alignment, :264); up and down
+                              must stay readable 16 bytes past their last offset */
   const int64_t* up_off;   /* [n_reads+1] */
   const uint8_t* down;     /* downstream flanks (:265) */
   const int64_t* down_off; /* [n_reads+1] */
@@ -104,7 +105,7 @@ enum {
   MPC_BUF_ROWMETA,      /* uint8[rows] bit0 odd position, bit1 first slot of its position */
   MPC_BUF_RIGHT_KEY,    /* uint32[n_reads_global] mixed downstream keys (multi-GPU exchange) */
   MPC_BUF_RIGHT_READ,   /* int32[n_reads_global] */
-  MPC_BUF_HASLEFT,      /* uint8[gaps] */
+  MPC_BUF_HASLEFT,      /* uint32[(gaps+31)/32 + 1] bitmap: gap holds a LEFT event */
   MPC_BUF_MAXR,         /* int32[gaps] */
   MPC_BUF_RUN_M,        /* int32[n_reads_global + gaps] */
   MPC_BUF_COUNT
@@ -135,6 +136,15 @@ int mpc_rows(mpc_plan* plan, void* stream);         /* depth, row assembly, flan
 int mpc_consensus(mpc_plan* plan, double min_depth_factor, double global_threshold_factor,
                   void* stream);                    /* max depth, calls, compaction            */
 int mpc_run(mpc_plan* plan, double min_depth_factor, double global_threshold_factor, void* stream);
+
+/* Measurement hook (bench.py): enqueue ONE launch of a single kernel with the
+ * same grid as inside the pipeline, so it can be bracketed by HIP events.
+ * The plan must have completed mpc_run() once; the status words are stale
+ * until the next mpc_run() (the long-insertion counter keeps growing). */
+#define MPC_K_PARSE 0
+#define MPC_K_LEFT 2
+#define MPC_K_STRINGS 3
+int mpc_profile_kernel(mpc_plan* plan, int which, void* stream);
 
 #ifdef __cplusplus
 }

@@ -61,6 +61,25 @@ __device__ __forceinline__ T wave_max(T v) {
   return v;
 }
 
+// ---- DPP wave64 scans (gfx9 row_shr / row_bcast; no LDS, no bpermute) ----
+template <int CTRL, int ROW_MASK = 0xf, int BANK_MASK = 0xf>
+__device__ __forceinline__ int dpp_i32(int v) {
+  return __builtin_amdgcn_update_dpp(0, v, CTRL, ROW_MASK, BANK_MASK, true);
+}
+// inclusive prefix sum over the 64 lanes (Kogge-Stone inside 16-lane rows, then
+// row_bcast:15 / row_bcast:31 to carry row totals)
+__device__ __forceinline__ int wave_scan_i32(int x) {
+  x += dpp_i32<0x111>(x);        // row_shr:1
+  x += dpp_i32<0x112>(x);        // row_shr:2
+  x += dpp_i32<0x114>(x);        // row_shr:4
+  x += dpp_i32<0x118>(x);        // row_shr:8
+  x += dpp_i32<0x142, 0xa>(x);   // row_bcast:15 -> rows 1, 3
+  x += dpp_i32<0x143, 0xc>(x);   // row_bcast:31 -> rows 2, 3
+  return x;
+}
+__device__ __forceinline__ int wave_last_i32(int x) { return __builtin_amdgcn_readlane(x, 63); }
+__device__ __forceinline__ int uniform_i32(int x) { return __builtin_amdgcn_readfirstlane(x); }
+
 __device__ __forceinline__ uint64_t ballot(bool p) { return (uint64_t)__ballot(p ? 1 : 0); }
 
 // Python str.strip() whitespace restricted to ASCII (the only bytes that can

@@ -21,7 +21,9 @@ DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL = 1, 2, 4, 8, 16, 32
 
 DE_NAMES = {DE_OP: "Unknown operator", DE_VALUE: "ValueError", DE_INDEX: "IndexError", DE_KEY: "KeyError",
             DE_CAPACITY: "row capacity", DE_INTERNAL: "internal invariant"}
+K_PARSE, K_ODD, K_LEFT, K_STRINGS = 0, 1, 2, 3
 CS_PAD = 2048  # readable bytes required past the end of the cs buffer (mpc.h)
+FLANK_PAD = 16  # readable bytes required past the end of the up/down buffers (mpc.h)
 
 
 class MpcError(RuntimeError):
@@ -79,6 +81,8 @@ def lib():
             getattr(L, f).argtypes = [vp, vp]
         L.mpc_consensus.argtypes = [vp, dbl, dbl, vp]
         L.mpc_run.argtypes = [vp, dbl, dbl, vp]
+        L.mpc_profile_kernel.argtypes = [vp, i32, vp]
+        L.mpc_profile_kernel.restype = i32
         for f in ("mpc_plan_create", "mpc_plan_destroy", "mpc_plan_workspace_bytes", "mpc_plan_bind",
                   "mpc_plan_buffer", "mpc_plan_set_input", "mpc_parse", "mpc_index", "mpc_tally",
                   "mpc_layout", "mpc_rows", "mpc_consensus", "mpc_run"):
@@ -151,8 +155,8 @@ class Batch:
 
         self.t = dict(
             ref=dev(ref), ref_off=dev(ref_off), cs=dev(cs, CS_PAD), cs_off=dev(cs_off),
-            tstart=dev(tstart.astype(np.int32)), up=dev(up), up_off=dev(up_off),
-            down=dev(dn), down_off=dev(dn_off), sample=dev(sample),
+            tstart=dev(tstart.astype(np.int32)), up=dev(up, FLANK_PAD), up_off=dev(up_off),
+            down=dev(dn, FLANK_PAD), down_off=dev(dn_off), sample=dev(sample),
         )
         self.h_cs_off = cs_off
         self.max_flank = int(max((np.diff(up_off).max() if len(up_off) > 1 else 0),
@@ -218,6 +222,9 @@ class Plan:
     def run(self, mdf, gtf, stream=None):
         _check(lib().mpc_run(self.h, float(mdf), float(gtf), self.stream_ptr(stream)))
 
+    def profile_kernel(self, which, stream=None):
+        _check(lib().mpc_profile_kernel(self.h, int(which), self.stream_ptr(stream)))
+
     def phase(self, name, stream=None, *args):
         fn = getattr(lib(), "mpc_" + name)
         if name == "consensus":
@@ -268,3 +275,31 @@ def pileup(samples, mdf, gtf, device=0, row_cap=None):
     res = plan.fetch()
     torch.cuda.synchronize(batch.device)
     return res
+
+
+class Runner:
+    """Repeated pileups over one device-resident Batch (bench / serving loop).
+    The first step sizes the row buffers exactly (re-plans once if needed)."""
+
+    def __init__(self, samples, device=0, row_cap=None):
+        self.batch = Batch(samples, device=device)
+        self.plan = Plan(self.batch, row_cap)
+        self._sized = False
+
+    def step(self, mdf, gtf, stream=None):
+        self.plan.run(mdf, gtf, stream)
+        if not self._sized:
+            st = self.plan.status()
+            flags = int(st[MPC_ST_FLAGS])
+            if flags & DE_CAPACITY and not (flags & ~DE_CAPACITY):
+                self.plan = Plan(self.batch, int(st[MPC_ST_ROWS_NEEDED]) + 16)
+                self.plan.run(mdf, gtf, stream)
+            self._sized = True
+
+    def check(self):
+        st = self.plan.status()
+        if int(st[MPC_ST_FLAGS]):
+            raise DataError(int(st[MPC_ST_FLAGS]), int(st[MPC_ST_FIRST_READ]))
+
+    def fetch(self):
+        return self.plan.fetch()

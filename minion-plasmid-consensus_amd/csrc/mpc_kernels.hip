@@ -130,26 +130,38 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int j) {
 // ---------------------------------------------------------------------------
 // K_parse: Step 4 of the reference (:285-323 tokenizer, :74-104 processOperation)
 // ---------------------------------------------------------------------------
-constexpr int kPW = 8;                 // waves per workgroup
-constexpr int kRB = 256;               // cs bytes staged per row per block step (16 lanes x 16 B)
-constexpr int kTPL = 4;                // tokens per lane per round (64 per row round; 4 rows <= kIB events)
-constexpr int kIB = 256;               // staged insertion events per wave
-constexpr int kRowBuf = kRB + 32;      // + room for 12-byte operand reads
-constexpr int kRowTok = kRB + 4;
-constexpr int kWaveLds = 4 * kRowBuf + 4 * 2 * kRowTok + 8 * kIB + 2 * 4 * 64 + 16;
+constexpr int kPW = 8;                  // waves per workgroup
+constexpr int kWin = 1024;              // window bytes (64 lanes x 16 B)
+constexpr int kStage = kWin + 128;      // + operand lookahead (halo, lanes 0..7)
+constexpr int kChunks = kStage / 16;
+constexpr int kHaloLanes = (kStage - kWin) / 16;
+constexpr int kSlots = 64;              // reads touching a window (slot 0 = read carried in)
+constexpr int kIB = 96;                 // staged insertion events per wave
+constexpr uint32_t kNoEnd = 0x7fffu;    // sentinel: next boundary lies beyond the halo
+
+struct WaveLds {                        // per-wave LDS of K_parse
+  int64_t s_val[kSlots];                // i = s_val + (window prefix of advances)
+  int64_t s_end[kSlots];                // cs offset of the read's end
+  uint64_t ibuf[kIB];
+  int32_t s_ts[kSlots], s_read[kSlots], s_iend[kSlots];  // s_iend bit 30: read has a downstream flank
+  uint8_t stage[kStage + 16];           // window + halo (+16: aligned word reads past the end)
+  uint16_t em[kChunks];                 // boundary bits: special characters | read starts
+  uint16_t ra[kChunks];                 // read-start bits
+  uint16_t tok[kWin + 2];               // token starts in [P, E), then the sentinel; bit 15 = read start
+};
 
 struct ParseArgs {  // slim argument block (no SGPR spills)
   const uint8_t* cs; const int64_t* cs_off; const int32_t* tstart;
   const int64_t* up_off; const int64_t* down_off; const int32_t* n_of; const int32_t* gbase;
   const int4* work;  // per workgroup: {sample, first read, end read, 0}
-  int64_t cs_base, ovf_cap, read_offset;
+  int64_t cs_base, ovf_cap, read_offset, n_reads;
   int32_t fused, nbmax;
   int32_t* i_end; uint64_t* ins_raw; uint64_t* ins_sorted; int32_t* bk_cnt; int32_t* bk_off; int64_t* rbase;
   Ovf* ovf; uint32_t* ovf_cnt; uint32_t* hasleft; uint32_t* status;
   int32_t* diff; uint32_t* sub;
 };
 
-__host__ __device__ constexpr int parse_stage_bytes() { return kPW * kWaveLds + 16; }
+__host__ __device__ constexpr int parse_stage_bytes() { return kPW * (int)sizeof(WaveLds) + 16; }
 __host__ __device__ inline int parse_hl_words(int n) { return (n + 1 + 31) / 32; }
 __host__ __device__ inline int parse_lds_bytes(int n_max, bool fused, int nbmax) {
   const int tallies = fused ? 12 * (n_max + 1) : 0;
@@ -157,118 +169,49 @@ __host__ __device__ inline int parse_lds_bytes(int n_max, bool fused, int nbmax)
   return parse_stage_bytes() + 4 * parse_hl_words(n_max) + (tallies > buckets ? tallies : buckets);
 }
 
-// DPP helpers on 16-lane rows
-template <int N>
-__device__ __forceinline__ int row_bcast(int v) { return __builtin_amdgcn_update_dpp(0, v, 0x150 + N, 0xf, 0xf, false); }
-__device__ __forceinline__ int row_scan(int x) {
-  x += dpp_i32<0x111>(x);
-  x += dpp_i32<0x112>(x);
-  x += dpp_i32<0x114>(x);
-  x += dpp_i32<0x118>(x);
-  return x;
-}
-
 struct TokInfo { int adv; int kind; uint32_t pay; uint32_t err; };
 
-// Semantics of one token that do not depend on its coordinate.  Operand bytes
-// are read as aligned LDS words and decoded SWAR-style (8 digits, 4 bases);
-// longer operands take a rare slow path.
-__device__ __forceinline__ TokInfo analyze_token(const uint8_t* buf, int sx, int ex, bool is_last) {
+// Semantics of one token that do not depend on its coordinate, operand read
+// from HBM: the slow path for rare tokens (operand past the staged halo, long
+// insertions, ':' operands that are not 1-4 plain digits).
+__device__ TokInfo analyze_long(const uint8_t* cs, int64_t s, int64_t e, bool is_last) {
   TokInfo r{0, 0, 0u, 0u};
-  const int olen = ex - sx - 1;
-  if (!(olen > 0 || is_last)) return r;  // empty operand: skipped unless last (:309, :320)
-  const uint32_t op = buf[sx];
-  const uint32_t* b32 = reinterpret_cast<const uint32_t*>(buf);
-  const int a = sx + 1;
-  const uint32_t q0 = b32[a >> 2], q1 = b32[(a >> 2) + 1];
-  const uint32_t w0 = __builtin_amdgcn_alignbyte(q1, q0, (uint32_t)(a & 3));
+  const uint32_t op = cs[s];
+  if (!is_special(op)) { r.err = DE_OP; return r; }
+  const int64_t olen = e - s - 1;
+  if (!(olen > 0 || is_last)) return r;
   if (op == ':') {
-    const uint32_t Tx = w0 ^ 0x30303030u;
-    const uint32_t nd = (((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u;
-    const uint32_t vm = olen >= 4 ? 0xffffffffu : ((1u << (8 * olen)) - 1u);
-    if (olen >= 1 && olen <= 4 && (nd & vm) == 0) {
-      // right-align up to 4 digits, then SWAR decimal conversion (pairs, quad)
-      uint32_t X = (Tx & vm & 0x0F0F0F0Fu) << (8 * (4 - olen));
-      X = (X * 2561u) >> 8;
-      X = ((X & 0x00FF00FFu) * 6553601u) >> 16;
-      r.adv = (int)(X & 0xffffu);
-    } else {
-      int64_t vv = 0;
-      if (!py_int(buf + a, (int64_t)olen, &vv)) r.err |= DE_VALUE;
-      else r.adv = vv <= 0 ? 0 : (vv < kAdvCap ? (int)vv : kAdvCap);
-    }
+    int64_t vv = 0;
+    if (!py_int(cs + s + 1, olen, &vv)) r.err |= DE_VALUE;
+    else r.adv = vv <= 0 ? 0 : (vv < kAdvCap ? (int)vv : kAdvCap);
     r.kind = r.adv > 0 ? 1 : 0;
   } else if (op == '*') {
-    if (olen == 0) { r.err |= DE_INDEX; return r; }  // operand[-1] of '' (:96)
-    const int cd = code_upper(buf[ex - 1]);
+    if (olen == 0) { r.err |= DE_INDEX; return r; }
+    const int cd = code_upper(cs[e - 1]);
     if (cd < 0) r.err |= DE_KEY;
-    r.pay = (uint32_t)(cd & 3);
-    r.adv = 1;
-    r.kind = 2;
+    r.pay = (uint32_t)(cd & 3); r.adv = 1; r.kind = 2;
   } else if (op == '+') {
     if (olen == 0) return r;
-    uint32_t packed = 0;
     bool ok = true;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int cd = code_upper((w0 >> (8 * k)) & 0xffu);
-      if (k < olen) { ok &= cd >= 0; packed |= (uint32_t)(cd & 3) << (2 * k); }
-    }
-    if (olen > 4)
-      for (int k = 4; k < olen; ++k) ok &= code_upper(buf[a + k]) >= 0;
+    for (int64_t x = s + 1; x < e; ++x) ok &= code_upper(cs[x]) >= 0;
     if (!ok) r.err |= DE_KEY;
-    r.pay = packed;
     r.kind = 3;
   } else if (op == '-') {
-    r.adv = olen < kAdvCap ? olen : kAdvCap;
+    r.adv = olen < kAdvCap ? (int)olen : kAdvCap;
     r.kind = olen > 0 ? 4 : 0;
-  } else if (op != 'Z') {
-    r.err |= DE_OP;
   }
   return r;
 }
 
-// Long-token fallback (operand longer than a row block), executed by one row:
-// the 16 lanes sweep HBM for the end of the operand.
-struct LongTok { int adv; int kind; int code; int64_t olen; int64_t end; uint32_t err; };
-__device__ LongTok long_token_row(const ParseArgs& a, int64_t pos, int64_t b1, int q, int rl) {
-  const uint32_t op = a.cs[pos];
-  const int64_t qq = pos + 1;
-  int64_t e = b1;
-  for (int64_t x = qq; x < b1; x += 16) {
-    const int64_t idx = x + rl;
-    const bool sp = idx < b1 && is_special(a.cs[idx]);
-    const uint32_t bal = (uint32_t)(ballot(sp) >> (16 * q)) & 0xffffu;
-    if (bal) { e = x + __ffs(bal) - 1; break; }
+// first special character in cs[x0, bound) (x0 16-aligned), else bound
+__device__ int64_t scan_special(const uint8_t* cs, int64_t x0, int64_t bound) {
+  for (int64_t x = x0; x < bound; x += 16) {
+    const uint4 v = *reinterpret_cast<const uint4*>(cs + x);
+    const int64_t lim = bound - x;
+    const uint32_t m = special_mask16(v, 0, lim > 16 ? 16 : (int)lim);
+    if (m) return x + __ffs(m) - 1;
   }
-  LongTok t{0, 0, 0, e - qq, e, 0u};
-  const int64_t olen = e - qq;
-  if (!(olen > 0 || e == b1)) return t;
-  if (op == '+') {
-    if (olen == 0) return t;
-    bool bad = false;
-    for (int64_t x = qq + rl; x < e; x += 16) bad |= code_upper(a.cs[x]) < 0;
-    if ((ballot(bad) >> (16 * q)) & 0xffffu) t.err |= DE_KEY;
-    t.kind = 3;
-  } else if (op == ':') {
-    int64_t vv = 0;
-    const bool ok = py_int(a.cs + qq, olen, &vv);  // every lane of the row, same answer
-    if (!ok) t.err |= DE_VALUE;
-    else if (vv > 0) { t.adv = vv < kAdvCap ? (int)vv : kAdvCap; t.kind = 1; }
-  } else if (op == '*') {
-    if (olen == 0) t.err |= DE_INDEX;
-    else {
-      const int cd = code_upper(a.cs[e - 1]);
-      if (cd < 0) t.err |= DE_KEY;
-      t.code = cd & 3; t.adv = 1; t.kind = 2;
-    }
-  } else if (op == '-') {
-    t.adv = olen < kAdvCap ? (int)olen : kAdvCap;
-    t.kind = olen > 0 ? 4 : 0;
-  } else if (op != 'Z') {
-    t.err |= DE_OP;
-  }
-  return t;
+  return bound;
 }
 
 __device__ __forceinline__ void push_ovf(const ParseArgs& a, int64_t off, int64_t r, int gap, int len) {
@@ -282,34 +225,68 @@ __device__ __forceinline__ void push_ovf(const ParseArgs& a, int64_t off, int64_
   }
 }
 
+__device__ __forceinline__ void flag_read(const ParseArgs& a, uint32_t err, int64_t r) {
+  atomicOr(&a.status[MPC_ST_FLAGS], err);
+  atomicMin(&a.status[MPC_ST_FIRST_READ], (uint32_t)r);
+}
+
 __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// Workgroup = contiguous reads of ONE sample (host work table).  A wave takes
-// batches of 64 consecutive reads (metadata loaded lane-parallel) and parses
-// FOUR reads at a time, one per 16-lane row: each row stages its read's cs in
-// 256-byte blocks, finds token starts with per-lane masks + a row DPP scan, and
-// each lane executes up to kTPL consecutive tokens per round, so one row DPP
-// scan of the lanes' advance sums gives every token its coordinate i.  No
-// global store happens inside the read loop: substitutions, deletions and read
-// spans are tallied in LDS (fused mode), insertion events are staged in a
-// per-wave LDS ring and LEFT-event gaps in an LDS bitmap.  At the end the
-// workgroup flushes its tallies and bucket-sorts its insertion events by gap.
+// inclusive wave prefix sum of values < 2^27 as int64 (two 32-bit DPP scans)
+__device__ __forceinline__ int64_t wave_scan_i64s(int v) {
+  const int lo = wave_scan_i32(v & 0xffff);
+  const int hi = wave_scan_i32(v >> 16);
+  return ((int64_t)hi << 16) + lo;
+}
+
+// One window's prefetched inputs: 16 cs bytes per lane (+16 halo bytes on
+// lanes < kHaloLanes) and the offsets / tstart of reads rs0 + lane.
+struct WinIn {
+  uint4 d, h;
+  int64_t o, uo, dno;
+  int32_t ts;
+};
+__device__ __forceinline__ WinIn fetch_window(const ParseArgs& a, int64_t P, int64_t rs0, int l) {
+  WinIn f;
+  const int64_t A = P & ~(int64_t)15;
+  f.d = *reinterpret_cast<const uint4*>(a.cs + A + 16 * l);
+  f.h = make_uint4(0, 0, 0, 0);
+  if (l < kHaloLanes) f.h = *reinterpret_cast<const uint4*>(a.cs + A + kWin + 16 * l);
+  const int64_t r = rs0 + l;
+  const bool ok = r <= a.n_reads;
+  f.o = ok ? a.cs_off[r] : INT64_MAX;
+  f.uo = ok ? a.up_off[r] : 0;
+  f.dno = ok ? a.down_off[r] : 0;
+  f.ts = r < a.n_reads ? a.tstart[r] : 0;
+  return f;
+}
+
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+// Workgroup = contiguous reads of ONE sample (host work table); wave w takes
+// the w-th eighth of them and streams their cs bytes in windows of 1 KiB
+// (16 B per lane, coalesced; the next window is loaded while this one is
+// processed).  Token boundaries (special characters and read starts) are bits
+// of an LDS mask; the token starts of a window are compacted into a list and
+// processed ONE TOKEN PER LANE, 64 per round: a mostly branch-free decode of the
+// operand word, one DPP scan of the advances for the coordinates i (reads are
+// segments: per-read bases in a slot table), ballot/mbcnt for the read slot and
+// the insertion-event index.  Effects: substitution / deletion / span tallies
+// (LDS), insertion events (per-wave LDS ring), LEFT-gap bits (LDS bitmap); no
+// global store inside the rounds.  Epilogue: flush tallies, bucket-sort
+// insertion events by gap.
+template <bool FUSED>
 __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int l = lane();
-  const int q = l >> 4, rl = l & 15;
   const int w = uniform_i32((int)(threadIdx.x >> 6));
-  uint8_t* wl = lds + w * kWaveLds;
-  uint8_t* buf = wl + q * kRowBuf;
-  uint16_t* tok = reinterpret_cast<uint16_t*>(wl + 4 * kRowBuf) + q * kRowTok;
-  uint64_t* ibuf = reinterpret_cast<uint64_t*>(wl + 4 * kRowBuf + 8 * kRowTok);
-  int32_t* res_iend = reinterpret_cast<int32_t*>(wl + 4 * kRowBuf + 8 * kRowTok + 8 * kIB);
-  uint32_t* res_err = reinterpret_cast<uint32_t*>(res_iend + 64);
-  uint32_t* rowerr = res_err + 64;  // [4]
+  WaveLds& W = *reinterpret_cast<WaveLds*>(lds + w * (int)sizeof(WaveLds));
   uint32_t* misc = reinterpret_cast<uint32_t*>(lds + parse_stage_bytes() - 16);  // [0] WG event count
   const int4 wk = a.work[blockIdx.x];
   const int smp = wk.x;
@@ -320,7 +297,7 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   uint8_t* uni = lds + parse_stage_bytes() + 4 * parse_hl_words(n);
   uint32_t* sub_l = reinterpret_cast<uint32_t*>(uni);                          // [2*(n+1)] 4 x u16
   int32_t* diff_l = reinterpret_cast<int32_t*>(sub_l + 2 * (n + 1));           // [n+1]
-  const bool fused = a.fused != 0;
+  constexpr bool fused = FUSED;  // tallies in LDS (one address space per instantiation)
   const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + r0;                   // insertion region
   const int64_t rb_cap = (a.cs_off[r1] - a.cs_base) / 2 + r1 - rb_wg;
   for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) hl[k] = 0;
@@ -329,6 +306,14 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   if (threadIdx.x == 0) misc[0] = 0;
   __syncthreads();
 
+  auto odd_sub = [&](int pos, int code) {
+    if (fused) atomicAdd(sub_l + 2 * pos + (code >> 1), 1u << (16 * (code & 1)));
+    else atomicAdd(a.sub + (int64_t)(gb + pos) * 4 + code, 1u);
+  };
+  auto odd_diff = [&](int pos, int v) {
+    if (fused) atomicAdd(diff_l + pos, v);
+    else atomicAdd(a.diff + gb + pos, v);
+  };
   int nib = 0;  // staged insertion events of this wave (wave-uniform)
   auto flush_ibuf = [&]() {
     wave_sync_lds();
@@ -338,240 +323,273 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
     if (basepos + nib > rb_cap) {
       if (l == 0) atomicOr(&a.status[MPC_ST_FLAGS], DE_INTERNAL);
     } else {
-      for (int k = l; k < nib; k += 64) a.ins_raw[rb_wg + basepos + k] = ibuf[k];
+      for (int k = l; k < nib; k += 64) a.ins_raw[rb_wg + basepos + k] = W.ibuf[k];
     }
     nib = 0;
   };
-  auto odd_sub = [&](int pos, int code) {
-    if (fused) atomicAdd(sub_l + 2 * pos + (code >> 1), 1u << (16 * (code & 1)));
-    else atomicAdd(a.sub + (int64_t)(gb + pos) * 4 + code, 1u);
-  };
-  auto odd_diff = [&](int pos, int v) {
-    if (fused) atomicAdd(diff_l + pos, v);
-    else atomicAdd(a.diff + gb + pos, v);
-  };
 
-  for (int64_t base = r0 + 64 * w; base < r1; base += 64 * kPW) {
-    const int nb = (int)(r1 - base < 64 ? r1 - base : 64);
-    // ---- batch metadata, lane j = read base+j ----
-    int64_t m_b0 = 0, m_b1 = 0;
-    int m_ts = 0, m_up = 0, m_dn = 0;
-    if (l < nb) {
-      const int64_t r = base + l;
-      m_b0 = a.cs_off[r]; m_b1 = a.cs_off[r + 1];
-      m_ts = a.tstart[r];
-      const int64_t u = a.up_off[r + 1] - a.up_off[r], dv = a.down_off[r + 1] - a.down_off[r];
-      m_up = u > 0x7fffffff ? 0x7fffffff : (int)u;
-      m_dn = dv > 0x7fffffff ? 0x7fffffff : (int)dv;
+  const int64_t ra = r0 + (r1 - r0) * w / kPW, rb = r0 + (r1 - r0) * (w + 1) / kPW;
+  const int64_t wend = a.cs_off[rb];
+  int64_t P = a.cs_off[ra];
+  int64_t rs0 = ra;         // first read whose cs starts at or after P
+  bool carry = false;       // slot 0 holds a read continuing into this window
+  WinIn cur = fetch_window(a, P, rs0, l);
+  while (P < wend) {
+    const int64_t A = P & ~(int64_t)15;
+    // ---- window end: at most 63 read starts in [P, E) ----
+    int64_t E = A + kWin < wend ? A + kWin : wend;
+    const int64_t o63 = readlane64(cur.o, 63);
+    if (o63 < E) E = o63;
+    const int64_t o_nx = __shfl(cur.o, (l + 1) & 63, 64);
+    const int64_t uo_nx = __shfl(cur.uo, (l + 1) & 63, 64);
+    const int64_t dno_nx = __shfl(cur.dno, (l + 1) & 63, 64);
+    if (E <= P) {
+      // reads rs0 .. rs0+62 all start at P: 63 empty cs (processOperation('', ''))
+      if (l < 63) {
+        flag_read(a, DE_OP, rs0 + l);
+        a.i_end[rs0 + l] = cur.ts < 0 ? 0 : (cur.ts > n ? n + 1 : cur.ts);
+      }
+      rs0 += 63;
+      cur = fetch_window(a, P, rs0, l);
+      continue;
     }
-    // ---- per-row read state (row-uniform values held by all 16 lanes) ----
-    int nxt = q;           // next batch index this row takes: q, q+4, ...
-    bool have = false;
-    int cur = 0;           // batch index of the row's current read
-    int64_t pos = 0, b1 = 0;
-    int i = 0, dn = 0;
-    uint32_t derr = 0;
-    bool first = false;
-    while (true) {
-      // rows without a read take their next one
-      // (the gather runs with the full exec mask: ds_bpermute returns 0 for
-      // inactive source lanes)
-      const bool take = !have && nxt < nb;
-      const int src = take ? nxt : l;
-      const int64_t g_b0 = __shfl(m_b0, src, 64);
-      const int64_t g_b1 = __shfl(m_b1, src, 64);
-      const int g_ts = __shfl(m_ts, src, 64);
-      const int g_up = __shfl(m_up, src, 64);
-      const int g_dn = __shfl(m_dn, src, 64);
-      if (take) {
-        cur = nxt;
-        nxt += 4;
-        const int64_t b0 = g_b0;
-        b1 = g_b1;
-        const int ts = g_ts;
-        const int up = g_up;
-        dn = g_dn;
-        derr = 0;
-        if (ts < 0) derr |= DE_INDEX;                   // deviation: no negative wrap
-        if (up > 0 && ts > n) derr |= DE_INDEX;         // leftIndel(2*i) past the end
-        if (up > 0 && ts >= 0 && ts <= n && rl == 0) atomicOr(hl + (ts >> 5), 1u << (ts & 31));
-        if (b1 <= b0) derr |= DE_OP;                    // processOperation('', '')
-        i = ts;
-        pos = b0;
-        first = true;
-        have = true;
-      }
-      if (!ballot(have)) break;
-      // ---- one 256-byte block step for every row with a read ----
-      const bool live = have && derr == 0 && pos < b1;
-      const int64_t apos = pos & ~(int64_t)15;
-      const int prel = (int)(pos - apos);
-      const int vend = live ? (int)((b1 < apos + kRB ? b1 : apos + kRB) - apos) : 0;
-      uint4 v = make_uint4(0, 0, 0, 0);
-      if (live) v = *reinterpret_cast<const uint4*>(a.cs + apos + 16 * rl);
-      *reinterpret_cast<uint4*>(buf + 16 * rl) = v;
-      const uint32_t mask = live ? special_mask16(v, prel - 16 * rl, vend - 16 * rl) : 0u;
-      const int cnt = __popc(mask);
-      const int incl = row_scan(cnt);
-      const int T = row_bcast<15>(incl);
-      {
-        int e = incl - cnt;
-        uint32_t m = mask;
-        while (m) {
-          const int k = __ffs(m) - 1;
-          m &= m - 1;
-          tok[e++] = (uint16_t)(16 * rl + k);
-        }
-      }
-      if (rl == 0) tok[T] = (uint16_t)vend;  // sentinel: end of the last token
-      wave_sync_lds();
-      const bool reaches_end = apos + kRB >= b1;
-      bool go = live;
-      if (go && first) {
-        // the reference runs processOperation('', operand) if the cs does not
-        // start with an operator -> sys.exit (:100-102)
-        if (T == 0 || tok[0] != (uint16_t)prel) { derr |= DE_OP; go = false; }
-        first = false;
-      }
-      const int Tproc = go ? (reaches_end ? T : T - 1) : 0;
-      const bool longtok = go && Tproc <= 0;
-      if (longtok) {
-        // ---- long token: its operand runs past this row block (rare) ----
-        const LongTok t = long_token_row(a, pos, b1, q, rl);
-        const int itok = i;
-        i = i + t.adv < kICap ? i + t.adv : kICap;
-        uint32_t te = t.err;
-        if (t.kind == 1 && (int64_t)itok + t.adv > n) te |= DE_INDEX;
-        if (t.kind == 2 && itok >= n) te |= DE_INDEX;
-        if (t.kind == 3 && itok > n) te |= DE_INDEX;
-        if (te == 0 && rl == 0) {
-          if (t.kind == 2) odd_sub(itok, t.code);
-          if (t.kind == 4 && itok < n) {
-            odd_diff(itok, -1);
-            odd_diff((int64_t)itok + t.olen < n ? (int)(itok + t.olen) : n, 1);
-          }
-          if (t.kind == 3) {
-            atomicOr(hl + (itok >> 5), 1u << (itok & 31));
-            push_ovf(a, pos + 1, base + cur, itok, (int)t.olen);
-          }
-        }
-        derr |= te;
-        pos = t.end;
-      }
-      // ---- rounds: lanes execute up to kTPL consecutive tokens each ----
-      const int64_t rg = a.read_offset + base + cur;
-      for (int t0 = 0; ballot(t0 < Tproc); t0 += 16 * kTPL) {
-        int Tr = Tproc - t0;
-        Tr = Tr < 0 ? 0 : (Tr > 16 * kTPL ? 16 * kTPL : Tr);
-        const int per = (Tr + 15) >> 4;
-        const int ta = t0 + rl * per;
-        int na = Tr - rl * per;
-        na = na < 0 ? 0 : (na > per ? per : na);
-        int pre[kTPL];
-        uint32_t inf[kTPL];
-        int lsum = 0, nins_l = 0;
-        uint32_t err = 0;
-#pragma unroll
-        for (int k = 0; k < kTPL; ++k) {
-          uint32_t info = 0;
-          int adv = 0;
-          if (k < na) {
-            const int t = ta + k;
-            const int sx = tok[t], ex = tok[t + 1];
-            const TokInfo ti = analyze_token(buf, sx, ex, reaches_end && t == T - 1);
-            const int olen = ex - sx - 1;
-            adv = ti.adv;
-            err |= ti.err;
-            info = (uint32_t)ti.kind | (ti.pay << 3) | ((uint32_t)olen << 11) | ((uint32_t)sx << 21);
-            nins_l += (ti.kind == 3 && olen <= kInsInline) ? 1 : 0;
-          }
-          pre[k] = lsum;
-          inf[k] = info;
-          lsum = lsum + adv < kLaneCap ? lsum + adv : kLaneCap;
-        }
-        const int rincl = row_scan(lsum);
-        const int ibase = i + rincl - lsum;
-        if (Tr > 0) {
-          const int tot = row_bcast<15>(rincl);
-          i = i + tot < kICap ? i + tot : kICap;
-        }
-        const int iin = wave_scan_i32(nins_l);
-        const int itot = wave_last_i32(iin);
-        if (nib + itot > kIB) flush_ibuf();
-        int iw = nib + iin - nins_l;
-        nib += itot;
-#pragma unroll
-        for (int k = 0; k < kTPL; ++k) {
-          if (k < na) {
-            const uint32_t info = inf[k];
-            const int kind = (int)(info & 7u);
-            const uint32_t pay = (info >> 3) & 0xffu;
-            const int olen = (int)((info >> 11) & 0x3ffu);
-            const int itok = ibase + pre[k];
-            const int adv = (k + 1 < na ? pre[k + 1] : lsum) - pre[k];
-            uint32_t te = 0;
-            if (kind == 1 && itok + adv > n) te |= DE_INDEX;
-            if (kind == 2 && itok >= n) te |= DE_INDEX;
-            if (kind == 3 && itok > n) te |= DE_INDEX;
-            err |= te;
-            if (te == 0) {
-              if (kind == 2) odd_sub(itok, (int)pay);
-              if (kind == 4 && itok < n) {
-                odd_diff(itok, -1);
-                odd_diff(itok + olen < n ? itok + olen : n, 1);
-              }
-              if (kind == 3) {
-                atomicOr(hl + (itok >> 5), 1u << (itok & 31));
-                if (olen > kInsInline) push_ovf(a, apos + (info >> 21) + 1, base + cur, itok, olen);
-              }
-            }
-            if (kind == 3 && olen <= kInsInline)
-              ibuf[iw++] = te == 0 ? ins_event(itok, olen, pay, rg) : ins_event((int)kNullGap, 1, 0u, rg);
-          }
-        }
-        if (ballot(err != 0)) {  // rare: fold the row's error bits together
-          if (l < 4) rowerr[l] = 0;
-          wave_sync_lds();
-          if (err) atomicOr(rowerr + q, err);
-          wave_sync_lds();
-          derr |= rowerr[q];
-        }
-      }
-      if (go && !longtok) pos = reaches_end ? b1 : apos + tok[T - 1];
-      // ---- rows whose read is complete (or failed) finish it ----
-      const bool done = have && (derr != 0 || pos >= b1);
-      if (done) {
-        if (derr == 0 && dn > 0 && i > n) derr |= DE_INDEX;  // rightIndel(2*i) past the end
-        if (rl == 0) {
-          res_iend[cur] = i < 0 ? 0 : (i > n ? n + 1 : i);
-          res_err[cur] = derr;
-        }
-        have = false;
-      }
+    const bool inwin = l < 63 && cur.o < E;  // read rs0+l starts in [P, E)
+    const int nst = __popcll(ballot(inwin));
+    // ---- stage bytes, boundary bits, per-read slots ----
+    *reinterpret_cast<uint4*>(W.stage + 16 * l) = cur.d;
+    W.em[l] = (uint16_t)special_mask16(cur.d, 0, 16);
+    W.ra[l] = 0;
+    if (l < kHaloLanes) {
+      *reinterpret_cast<uint4*>(W.stage + kWin + 16 * l) = cur.h;
+      W.em[64 + l] = (uint16_t)special_mask16(cur.h, 0, 16);
+      W.ra[64 + l] = 0;
+    }
+    if (inwin) {
+      const int q = l + 1;
+      const int64_t up = uo_nx - cur.uo, dn = dno_nx - cur.dno;
+      const int ts = cur.ts;
+      uint32_t derr = 0;
+      if (ts < 0) derr |= DE_INDEX;                   // deviation: no negative wrap
+      if (up > 0 && ts > n) derr |= DE_INDEX;         // leftIndel(2*i) past the end
+      if (o_nx <= cur.o) derr |= DE_OP;               // processOperation('', '')
+      if (derr) flag_read(a, derr, rs0 + l);
+      if (up > 0 && ts >= 0 && ts <= n) atomicOr(hl + (ts >> 5), 1u << (ts & 31));
+      W.s_end[q] = o_nx;
+      W.s_ts[q] = ts < 0 ? -1 : (ts > kICap ? kICap : ts);
+      W.s_read[q] = (int32_t)(rs0 + l);
+      W.s_iend[q] = (ts < 0 ? 0 : (ts > n ? n + 1 : ts)) | (dn > 0 ? 1 << 30 : 0);
     }
     wave_sync_lds();
-    // ---- per-read results, lane-parallel ----
-    int m_iend = 0;
-    uint32_t m_err = 0;
-    if (l < nb) {
-      const int64_t r = base + l;
-      m_iend = res_iend[l];
-      m_err = res_err[l];
-      a.i_end[r] = m_iend;
-      if (m_err) {
-        atomicOr(&a.status[MPC_ST_FLAGS], m_err);
-        atomicMin(&a.status[MPC_ST_FIRST_READ], (uint32_t)r);
+    {  // read-start bits of every known start in the stage
+      const int64_t rel = cur.o - A;
+      if (rel >= 0 && rel < kStage) {
+        atomicOr(reinterpret_cast<uint32_t*>(W.em) + (rel >> 5), 1u << (rel & 31));
+        atomicOr(reinterpret_cast<uint32_t*>(W.ra) + (rel >> 5), 1u << (rel & 31));
       }
     }
-    // read span [tstart, min(i_end, n)) -> depth difference points
-    const int e = m_iend > n ? n : m_iend;
-    const bool span = l < nb && m_err == 0 && m_ts >= 0 && m_ts < e;
-    if (fused) {
-      if (span) { atomicAdd(diff_l + m_ts, 1); atomicAdd(diff_l + e, -1); }
-    } else {
-      peel_atomic_add(a.diff, (int64_t)gb + m_ts, 1, span);
-      peel_atomic_add(a.diff, (int64_t)gb + e, -1, span);
+    // ---- prefetch the next window ----
+    const int64_t Pn = E, rsn = rs0 + nst;
+    WinIn nxt;
+    if (Pn < wend) nxt = fetch_window(a, Pn, rsn, l);
+    wave_sync_lds();
+
+    // ---- token list: starts in [P, E) (bit 15 = read start), then the sentinel ----
+    const int64_t cA = A + 16 * l;
+    const uint32_t em_own = W.em[l];
+    const uint32_t ra_own = W.ra[l];
+    int T;
+    {
+      int tlo = (int)(P - cA), thi = (int)(E - cA < 16 ? E - cA : 16);
+      tlo = tlo < 0 ? 0 : (tlo > 16 ? 16 : tlo);
+      thi = thi < 0 ? 0 : thi;
+      const uint32_t tm = em_own & ((1u << thi) - 1u) & ~((1u << tlo) - 1u);
+      const int cnt = __popc(tm);
+      const int incl = wave_scan_i32(cnt);
+      T = wave_last_i32(incl);
+      int idx = incl - cnt;
+      uint32_t m = tm;
+      while (m) {
+        const int k = __ffs(m) - 1;
+        m &= m - 1;
+        W.tok[idx++] = (uint16_t)((16 * l + k) | (((ra_own >> k) & 1u) << 15));
+      }
+      // first boundary at or after E: ends the window's last token
+      const int sh = (int)(E - cA);
+      const uint32_t sb = sh >= 16 ? 0u : (sh <= 0 ? em_own : em_own & ~((1u << sh) - 1u));
+      uint64_t bal = ballot(sb != 0);
+      uint32_t sent = kNoEnd;
+      if (bal) {
+        const int f = __ffsll((unsigned long long)bal) - 1;
+        const uint32_t bf = (uint32_t)__builtin_amdgcn_readlane((int)sb, f);
+        const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)ra_own, f);
+        const int k = __ffs(bf) - 1;
+        sent = (uint32_t)(16 * f + k) | (((rf >> k) & 1u) << 15);
+      } else {
+        const uint32_t hb = l < kHaloLanes ? W.em[64 + l] : 0u;
+        const uint32_t hr = l < kHaloLanes ? W.ra[64 + l] : 0u;
+        bal = ballot(hb != 0);
+        if (bal) {
+          const int f = __ffsll((unsigned long long)bal) - 1;
+          const uint32_t bf = (uint32_t)__builtin_amdgcn_readlane((int)hb, f);
+          const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)hr, f);
+          const int k = __ffs(bf) - 1;
+          sent = (uint32_t)(kWin + 16 * f + k) | (((rf >> k) & 1u) << 15);
+        }
+      }
+      if (l == 0) W.tok[T] = (uint16_t)sent;
     }
+    wave_sync_lds();
+
+    // ---- rounds: one token per lane ----
+    int64_t G = 0;  // advances of the window's earlier rounds
+    int qc = 0;     // read starts of the window's earlier rounds
+    for (int t0 = 0; t0 < T; t0 += 64) {
+      if (nib + 64 > kIB) flush_ibuf();
+      const int t = t0 + l;
+      const bool v = t < T;
+      const uint32_t e0 = v ? W.tok[t] : 0u, e1 = v ? W.tok[t + 1] : 0u;
+      const int sx = (int)(e0 & 0x7fffu);
+      const int ex = (int)(e1 & 0x7fffu);
+      const bool is_rs = v && (e0 >> 15);
+      bool last = v && (e1 >> 15);
+      const uint64_t brs = ballot(is_rs);
+      const int q = qc + lanes_below(brs) + (is_rs ? 1 : 0);
+      // fast decode from the staged bytes
+      const uint32_t op = W.stage[sx];
+      const int ao = sx + 1;
+      const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage);
+      const uint32_t w0 = __builtin_amdgcn_alignbyte(b32[(ao >> 2) + 1], b32[ao >> 2], (uint32_t)(ao & 3));
+      bool slow = v && ex == (int)kNoEnd;
+      int olen = ex - sx - 1;
+      uint32_t err = 0, pay = 0;
+      int kind = 0, adv = 0;
+      if (v && !slow) {
+        if (!is_special(op)) {
+          err = DE_OP;  // cs does not start with an operator (:100-102)
+        } else if (olen > 0 || last) {  // empty operand: skipped unless last (:309, :320)
+          if (op == ':') {
+            const uint32_t Tx = w0 ^ 0x30303030u;
+            const uint32_t nd = (((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u;
+            const uint32_t vm = olen >= 4 ? 0xffffffffu : ((1u << (8 * olen)) - 1u);
+            if (olen >= 1 && olen <= 4 && (nd & vm) == 0) {
+              // right-align up to 4 digits, then SWAR decimal conversion (pairs, quad)
+              uint32_t X = (Tx & vm & 0x0F0F0F0Fu) << (8 * (4 - olen));
+              X = (X * 2561u) >> 8;
+              X = ((X & 0x00FF00FFu) * 6553601u) >> 16;
+              adv = (int)(X & 0xffffu);
+              kind = adv > 0 ? 1 : 0;
+            } else {
+              slow = true;  // int() of a longer / unusual operand
+            }
+          } else if (op == '*') {
+            if (olen == 0) err = DE_INDEX;  // operand[-1] of '' (:96)
+            else if (olen <= 4) {
+              const int cd = code_upper((w0 >> (8 * (olen - 1))) & 0xffu);
+              if (cd < 0) err = DE_KEY;
+              pay = (uint32_t)(cd & 3);
+              adv = 1;
+              kind = 2;
+            } else {
+              slow = true;
+            }
+          } else if (op == '+') {
+            if (olen > kInsInline) slow = true;  // long insertion
+            else if (olen > 0) {
+              bool ok = true;
+#pragma unroll
+              for (int k = 0; k < 4; ++k) {
+                const int cd = code_upper((w0 >> (8 * k)) & 0xffu);
+                if (k < olen) { ok &= cd >= 0; pay |= (uint32_t)(cd & 3) << (2 * k); }
+              }
+              if (!ok) err = DE_KEY;
+              kind = 3;
+            }
+          } else if (op == '-') {
+            adv = olen < kAdvCap ? olen : kAdvCap;
+            kind = 4;
+          }
+        }
+      }
+      if (slow) {  // rare: decode from HBM
+        const int64_t s = A + sx;
+        int64_t e = A + ex;
+        if (ex == (int)kNoEnd) {
+          const int64_t send = W.s_end[q];
+          e = scan_special(a.cs, A + kStage, send);
+          last = e == send;
+        }
+        const TokInfo ti = analyze_long(a.cs, s, e, last);
+        adv = ti.adv; kind = ti.kind; pay = ti.pay; err = ti.err;
+        olen = (int)(e - s - 1 < kAdvCap ? e - s - 1 : kAdvCap);
+      }
+      // ---- coordinates ----
+      const int ainc = wave_scan_i32(adv);  // adv <= 2^22: 64 lanes stay < 2^31
+      const int aex = ainc - adv;
+      const int atot = wave_last_i32(ainc);
+      if (is_rs) W.s_val[q] = (int64_t)W.s_ts[q] - (G + aex);
+      wave_sync_lds();
+      const int64_t i64 = W.s_val[q] + G + aex;
+      const int itok = (int)(i64 < -(1 << 30) ? -(1 << 30) : (i64 > kICap ? kICap : i64));
+      // ---- effects ----
+      uint32_t te = err;
+      if (kind == 1 && (int64_t)itok + adv > n) te |= DE_INDEX;
+      if (kind == 2 && itok >= n) te |= DE_INDEX;
+      if (kind == 3 && itok > n) te |= DE_INDEX;
+      const int64_t rl = W.s_read[q];
+      const bool ins_inline = kind == 3 && olen <= kInsInline;
+      const uint64_t bins = ballot(ins_inline);
+      if (te == 0) {
+        if (kind == 2) odd_sub(itok, (int)pay);
+        if (kind == 4 && itok >= 0 && itok < n) {
+          odd_diff(itok, -1);
+          odd_diff((int64_t)itok + olen < n ? itok + olen : n, 1);
+        }
+        if (kind == 3) {
+          atomicOr(hl + (itok >> 5), 1u << (itok & 31));
+          if (olen > kInsInline) push_ovf(a, A + sx + 1, rl, itok, olen);
+        }
+      }
+      if (ins_inline)
+        W.ibuf[nib + lanes_below(bins)] = te == 0 ? ins_event(itok, olen, pay, a.read_offset + rl)
+                                                 : ins_event((int)kNullGap, 1, 0u, a.read_offset + rl);
+      if (last) {  // the read's last operation: i_end, downstream check, span
+        const int64_t ia = i64 + adv;
+        const int ie = (int)(ia < 0 ? 0 : (ia > n ? n + 1 : ia));
+        const int dnf = W.s_iend[q] & (1 << 30);
+        if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
+        W.s_iend[q] = ie | dnf;
+        const int ts = W.s_ts[q];
+        const int e2 = ie > n ? n : ie;
+        if (ts >= 0 && ts < e2) { odd_diff(ts, 1); odd_diff(e2, -1); }
+      }
+      if (te) flag_read(a, te, rl);
+      G += atot;
+      qc += __popcll(brs);
+      nib += __popcll(bins);
+    }
+    wave_sync_lds();
+    // ---- reads that ended in this window: i_end; carry the open one ----
+    if (l <= nst && (l > 0 || carry) && W.s_end[l] <= E) a.i_end[W.s_read[l]] = W.s_iend[l] & ~(1 << 30);
+    const bool cont = (nst > 0 || carry) && W.s_end[nst] > E;
+    if (cont && l == 0) {
+      const int64_t v = W.s_val[nst] + G;
+      W.s_val[0] = v > kICap ? kICap : v;
+      W.s_end[0] = W.s_end[nst];
+      W.s_ts[0] = W.s_ts[nst];
+      W.s_read[0] = W.s_read[nst];
+      W.s_iend[0] = W.s_iend[nst];
+    }
+    carry = cont;
+    wave_sync_lds();
+    P = Pn;
+    rs0 = rsn;
+    if (Pn < wend) cur = nxt;
+  }
+  // reads starting at the range end have an empty cs
+  for (int64_t r = rs0 + l; r < rb; r += 64) {
+    const int ts = a.tstart[r];
+    flag_read(a, DE_OP, r);
+    a.i_end[r] = ts < 0 ? 0 : (ts > n ? n + 1 : ts);
   }
   if (nib) flush_ibuf();
   __syncthreads();
@@ -600,31 +618,31 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   const int nbk = (n + 1 + kBW - 1) / kBW;
   uint32_t* bcnt = reinterpret_cast<uint32_t*>(uni);  // aliases the (flushed) tallies
   uint32_t* bcur = bcnt + nbk;
-  const int E = (int)misc[0];
+  const int Ev = (int)misc[0];
   for (int k = threadIdx.x; k < nbk; k += blockDim.x) bcnt[k] = 0;
   __syncthreads();
-  for (int k = threadIdx.x; k < E; k += blockDim.x) {
+  for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
     const uint32_t gap = (uint32_t)(a.ins_raw[rb_wg + k] >> 10) & kNullGap;
     if (gap <= (uint32_t)n) atomicAdd(bcnt + gap / kBW, 1u);
   }
   __syncthreads();
   if (threadIdx.x < 64) {  // exclusive scan over buckets by one wave
-    int carry = 0;
+    int carry_b = 0;
     for (int c0 = 0; c0 < nbk; c0 += 64) {
       const int k = c0 + l;
       const int v = k < nbk ? (int)bcnt[k] : 0;
       const int inc = wave_scan_i32(v);
       if (k < nbk) {
-        bcur[k] = (uint32_t)(carry + inc - v);
+        bcur[k] = (uint32_t)(carry_b + inc - v);
         a.bk_cnt[(int64_t)blockIdx.x * a.nbmax + k] = v;
-        a.bk_off[(int64_t)blockIdx.x * a.nbmax + k] = carry + inc - v;
+        a.bk_off[(int64_t)blockIdx.x * a.nbmax + k] = carry_b + inc - v;
       }
-      carry += wave_last_i32(inc);
+      carry_b += wave_last_i32(inc);
     }
   }
   if (threadIdx.x == 0) a.rbase[blockIdx.x] = rb_wg;
   __syncthreads();
-  for (int k = threadIdx.x; k < E; k += blockDim.x) {
+  for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
     const uint64_t ev = a.ins_raw[rb_wg + k];
     const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
     if (gap <= (uint32_t)n) a.ins_sorted[rb_wg + atomicAdd(bcur + gap / kBW, 1u)] = ev;
@@ -1252,7 +1270,7 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.cs = d.cs; a.cs_off = d.cs_off; a.tstart = d.tstart; a.up_off = d.up_off; a.down_off = d.down_off;
   a.n_of = d.n_of; a.gbase = d.gbase;
   a.work = reinterpret_cast<const int4*>(p->ws + p->off[mpc_plan::B_WPARSE]);
-  a.cs_base = d.cs_base; a.ovf_cap = d.ovf_cap; a.read_offset = d.read_offset;
+  a.cs_base = d.cs_base; a.ovf_cap = d.ovf_cap; a.read_offset = d.read_offset; a.n_reads = d.N;
   a.fused = p->fused ? 1 : 0; a.nbmax = p->nbmax;
   a.i_end = d.i_end;
   a.ins_raw = at<uint64_t>(p, mpc_plan::B_INSRAW); a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
@@ -1261,6 +1279,13 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.hasleft = d.hasleft; a.status = d.status;
   a.diff = d.diff; a.sub = d.sub;
   return a;
+}
+
+static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
+  if (p->fused)
+    hipLaunchKernelGGL(K_parse<true>, dim3(p->n_parse_wg), dim3(kPW * 64), p->parse_lds, st, parse_args(p, d));
+  else
+    hipLaunchKernelGGL(K_parse<false>, dim3(p->n_parse_wg), dim3(kPW * 64), p->parse_lds, st, parse_args(p, d));
 }
 
 static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
@@ -1353,6 +1378,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       if (ns <= 0) continue;
       int64_t ch = std::max<int64_t>(1, (target * ns + std::max<int64_t>(p->N, 1) - 1) / std::max<int64_t>(p->N, 1));
       ch = std::min<int64_t>(ch, (ns + 63) / 64);
+      ch = std::max<int64_t>(ch, (ns + 65534) / 65535);  // LDS substitution tallies are 16-bit
       for (int64_t c = 0; c < ch; ++c) {
         const int64_t x = a + ns * c / ch, y = a + ns * (c + 1) / ch;
         if (y > x) p->work_parse.insert(p->work_parse.end(), {s, (int32_t)x, (int32_t)y, 0});
@@ -1467,7 +1493,8 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WPARSE), p->work_parse.data(), 4 * p->work_parse.size(), hipMemcpyHostToDevice));
   if (!p->work_left.empty())
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WLEFT), p->work_left.data(), 4 * p->work_left.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipFuncSetAttribute((const void*)K_parse, hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
+  HIPCHK(hipFuncSetAttribute((const void*)K_parse<true>, hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
+  HIPCHK(hipFuncSetAttribute((const void*)K_parse<false>, hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
   p->bound = true;
   return MPC_OK;
 }
@@ -1507,7 +1534,7 @@ int mpc_parse(mpc_plan* p, void* stream) {
   HIPCHK(hipMemsetAsync(d.diff, 0, 4 * p->G, st));
   HIPCHK(hipMemsetAsync(d.sub, 0, 16 * p->G, st));
   if (p->n_parse_wg > 0)
-    hipLaunchKernelGGL(K_parse, dim3(p->n_parse_wg), dim3(kPW * 64), p->parse_lds, st, parse_args(p, d));
+    launch_parse(p, d, st);
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -1596,7 +1623,7 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
   if (p->N == 0) return MPC_OK;
   switch (which) {
     case MPC_K_PARSE:  // re-adds the odd tallies: status/tallies are stale until the next mpc_run
-      hipLaunchKernelGGL(K_parse, dim3(p->n_parse_wg), dim3(kPW * 64), p->parse_lds, st, parse_args(p, d));
+      launch_parse(p, d, st);
       break;
     case MPC_K_LEFT:
       hipLaunchKernelGGL(K_left, dim3(p->n_left_wg), dim3(256), 0, st, left_args(p, d));

@@ -61,6 +61,7 @@ extern "C" {
 #define MPC_ST_FIRST_READ 1  /* smallest local read index with a data error (0xFFFFFFFF if none) */
 #define MPC_ST_ROWS_NEEDED 2 /* rows (pileup slots incl. empty odd positions) the layout needs */
 #define MPC_ST_MIXED 3       /* downstream (RIGHT) events at gaps that also hold LEFT events */
+#define MPC_ST_UNITS 4       /* internal: work units of the bucketed event tallies */
 #define MPC_ST_WORDS 8
 
 /* Per-read inputs, already in HBM.  One sample = one (assembly, PAF) pair, e.g.
@@ -143,7 +144,7 @@ int mpc_run(mpc_plan* plan, double min_depth_factor, double global_threshold_fac
  * until the next mpc_run() (the long-insertion counter keeps growing). */
 #define MPC_K_PARSE 0
 #define MPC_K_LEFT 2
-#define MPC_K_STRINGS 3
+#define MPC_K_FLANK 3
 int mpc_profile_kernel(mpc_plan* plan, int which, void* stream);
 
 #ifdef __cplusplus

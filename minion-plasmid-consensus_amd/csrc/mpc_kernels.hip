@@ -18,7 +18,7 @@
 //                           processBaseString_* (:37-72), row offsets (scan)
 //   rows      scan          depth = prefix(difference array)
 //             K_assemble    odd rows + F -> rows (plain stores)
-//             K_strings     flanks + long insertions -> rows (LDS hash)
+//             K_flank       flanks (per gap bucket, dense LDS rows) + long insertions
 //   consensus K_call        per-slot top/second/tie/N (:363-439), max depth
 //             scan, K_emit  threshold test + ordered compaction of the calls
 #include <hip/hip_runtime.h>
@@ -51,7 +51,7 @@ constexpr int kBW = 16;             // gaps per insertion bucket (K_left workgro
 constexpr int kKMax = 8;            // runs per gap tallied in K_left's LDS (others go to HBM)
 constexpr uint32_t kNullGap = 0x3fffffu;
 
-struct Ovf {  // long insertion (len > kInsInline), tallied by K_strings
+struct Ovf {  // long insertion (len > kInsInline), tallied by K_flank
   int64_t off;  // absolute byte offset of the inserted bases in cs
   int32_t read;
   int32_t gap;  // local gap index (i), sample implied by read
@@ -64,6 +64,14 @@ struct Ovf {  // long insertion (len > kInsInline), tallied by K_strings
 __device__ __forceinline__ uint64_t ins_event(int gap, int len, uint32_t bases, int64_t rg) {
   return ((uint64_t)(uint32_t)rg << 32) | ((uint32_t)gap << 10) | ((uint32_t)(len - 1) << 8) | bases;
 }
+// flank event: bit 63 set, bit 62 = downstream (RIGHT) flank, bits 32..61 =
+// global read, gap << 10.  Bucket-sorted with the insertion events (separate
+// buckets) so K_left / K_flank find the flanks anchored at their gaps.
+constexpr uint64_t kFlankBit = 1ull << 63, kDownBit = 1ull << 62;
+__device__ __forceinline__ uint64_t flank_event(int gap, bool down, int64_t rg) {
+  return kFlankBit | (down ? kDownBit : 0ull) | ((uint64_t)((uint32_t)rg & 0x3fffffffu) << 32) | ((uint32_t)gap << 10);
+}
+__device__ __forceinline__ int64_t event_read(uint64_t ev) { return (int64_t)((ev >> 32) & 0x3fffffffu); }
 
 struct Dev {  // device-side views of the plan for the small kernels (passed by value)
   const uint8_t* ref; const int64_t* ref_off;
@@ -82,6 +90,7 @@ struct Dev {  // device-side views of the plan for the small kernels (passed by 
   int32_t* maxR;
   uint32_t* keys_in; int32_t* vals_in; uint32_t* keys_out; int32_t* vals_out;
   int32_t* rlen;                     // [Ng] downstream length by global read
+  int32_t* rpos;                     // [N] local read -> position of its mixed RIGHT event in the sorted list
   int32_t* right_start;              // [G+1]
   int32_t* diff;                     // [G]
   uint32_t* sub;                     // [G][4]
@@ -155,7 +164,7 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
   const int64_t* up_off; const int64_t* down_off; const int32_t* n_of; const int32_t* gbase;
   const int4* work;  // per workgroup: {sample, first read, end read, 0}
   int64_t cs_base, ovf_cap, read_offset, n_reads;
-  int32_t fused, nbmax;
+  int32_t fused, nbs;  // nbs: bucket slots per parse workgroup (2 x max buckets)
   int32_t* i_end; uint64_t* ins_raw; uint64_t* ins_sorted; int32_t* bk_cnt; int32_t* bk_off; int64_t* rbase;
   Ovf* ovf; uint32_t* ovf_cnt; uint32_t* hasleft; uint32_t* status;
   int32_t* diff; uint32_t* sub;
@@ -165,7 +174,7 @@ __host__ __device__ constexpr int parse_stage_bytes() { return kPW * (int)sizeof
 __host__ __device__ inline int parse_hl_words(int n) { return (n + 1 + 31) / 32; }
 __host__ __device__ inline int parse_lds_bytes(int n_max, bool fused, int nbmax) {
   const int tallies = fused ? 12 * (n_max + 1) : 0;
-  const int buckets = 8 * nbmax;
+  const int buckets = 16 * nbmax;  // counts + cursors, insertion and flank buckets
   return parse_stage_bytes() + 4 * parse_hl_words(n_max) + (tallies > buckets ? tallies : buckets);
 }
 
@@ -298,8 +307,8 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   uint32_t* sub_l = reinterpret_cast<uint32_t*>(uni);                          // [2*(n+1)] 4 x u16
   int32_t* diff_l = reinterpret_cast<int32_t*>(sub_l + 2 * (n + 1));           // [n+1]
   constexpr bool fused = FUSED;  // tallies in LDS (one address space per instantiation)
-  const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + r0;                   // insertion region
-  const int64_t rb_cap = (a.cs_off[r1] - a.cs_base) / 2 + r1 - rb_wg;
+  const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;               // event region
+  const int64_t rb_cap = (a.cs_off[r1] - a.cs_base) / 2 + 3 * r1 - rb_wg;
   for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) hl[k] = 0;
   if (fused)
     for (int k = threadIdx.x; k < 3 * (n + 1); k += blockDim.x) sub_l[k] = 0;
@@ -364,6 +373,8 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       W.em[64 + l] = (uint16_t)special_mask16(cur.h, 0, 16);
       W.ra[64 + l] = 0;
     }
+    if (nib + 64 > kIB) flush_ibuf();
+    bool lflank = false;
     if (inwin) {
       const int q = l + 1;
       const int64_t up = uo_nx - cur.uo, dn = dno_nx - cur.dno;
@@ -373,11 +384,19 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       if (up > 0 && ts > n) derr |= DE_INDEX;         // leftIndel(2*i) past the end
       if (o_nx <= cur.o) derr |= DE_OP;               // processOperation('', '')
       if (derr) flag_read(a, derr, rs0 + l);
-      if (up > 0 && ts >= 0 && ts <= n) atomicOr(hl + (ts >> 5), 1u << (ts & 31));
+      if (up > 0 && ts >= 0 && ts <= n) {
+        atomicOr(hl + (ts >> 5), 1u << (ts & 31));
+        lflank = true;
+      }
       W.s_end[q] = o_nx;
       W.s_ts[q] = ts < 0 ? -1 : (ts > kICap ? kICap : ts);
       W.s_read[q] = (int32_t)(rs0 + l);
       W.s_iend[q] = (ts < 0 ? 0 : (ts > n ? n + 1 : ts)) | (dn > 0 ? 1 << 30 : 0);
+    }
+    {  // upstream flank = LEFT event at gap tstart
+      const uint64_t bl = ballot(lflank);
+      if (lflank) W.ibuf[nib + lanes_below(bl)] = flank_event(cur.ts, false, a.read_offset + rs0 + l);
+      nib += __popcll(bl);
     }
     wave_sync_lds();
     {  // read-start bits of every known start in the stage
@@ -459,57 +478,39 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       const int ao = sx + 1;
       const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage);
       const uint32_t w0 = __builtin_amdgcn_alignbyte(b32[(ao >> 2) + 1], b32[ao >> 2], (uint32_t)(ao & 3));
-      bool slow = v && ex == (int)kNoEnd;
       int olen = ex - sx - 1;
-      uint32_t err = 0, pay = 0;
-      int kind = 0, adv = 0;
-      if (v && !slow) {
-        if (!is_special(op)) {
-          err = DE_OP;  // cs does not start with an operator (:100-102)
-        } else if (olen > 0 || last) {  // empty operand: skipped unless last (:309, :320)
-          if (op == ':') {
-            const uint32_t Tx = w0 ^ 0x30303030u;
-            const uint32_t nd = (((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u;
-            const uint32_t vm = olen >= 4 ? 0xffffffffu : ((1u << (8 * olen)) - 1u);
-            if (olen >= 1 && olen <= 4 && (nd & vm) == 0) {
-              // right-align up to 4 digits, then SWAR decimal conversion (pairs, quad)
-              uint32_t X = (Tx & vm & 0x0F0F0F0Fu) << (8 * (4 - olen));
-              X = (X * 2561u) >> 8;
-              X = ((X & 0x00FF00FFu) * 6553601u) >> 16;
-              adv = (int)(X & 0xffffu);
-              kind = adv > 0 ? 1 : 0;
-            } else {
-              slow = true;  // int() of a longer / unusual operand
-            }
-          } else if (op == '*') {
-            if (olen == 0) err = DE_INDEX;  // operand[-1] of '' (:96)
-            else if (olen <= 4) {
-              const int cd = code_upper((w0 >> (8 * (olen - 1))) & 0xffu);
-              if (cd < 0) err = DE_KEY;
-              pay = (uint32_t)(cd & 3);
-              adv = 1;
-              kind = 2;
-            } else {
-              slow = true;
-            }
-          } else if (op == '+') {
-            if (olen > kInsInline) slow = true;  // long insertion
-            else if (olen > 0) {
-              bool ok = true;
-#pragma unroll
-              for (int k = 0; k < 4; ++k) {
-                const int cd = code_upper((w0 >> (8 * k)) & 0xffu);
-                if (k < olen) { ok &= cd >= 0; pay |= (uint32_t)(cd & 3) << (2 * k); }
-              }
-              if (!ok) err = DE_KEY;
-              kind = 3;
-            }
-          } else if (op == '-') {
-            adv = olen < kAdvCap ? olen : kAdvCap;
-            kind = 4;
-          }
-        }
-      }
+      // branch-free decode: op class, 4 operand bytes at once (SWAR)
+      const bool colon = op == ':', star = op == '*', plus = op == '+', minus = op == '-';
+      const bool spec = colon | star | plus | minus | (op == 'Z');
+      const bool act = v & spec & ((olen > 0) | last);  // empty operand: skipped unless last (:309, :320)
+      const int ol4 = olen < 0 ? 0 : (olen > 4 ? 4 : olen);
+      const uint32_t vm = ol4 == 4 ? 0xffffffffu : ((1u << (8 * ol4)) - 1u);  // operand bytes in w0
+      //   ':' up to 4 digits -> right-align, SWAR decimal conversion (pairs, quad)
+      const uint32_t Tx = w0 ^ 0x30303030u;
+      const uint32_t nd = (((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u;
+      const bool dig_ok = (olen >= 1) & (olen <= 4) & ((nd & vm) == 0);
+      uint32_t X = (Tx & vm & 0x0F0F0F0Fu) << (8 * (4 - ol4));
+      X = (X * 2561u) >> 8;
+      X = ((X & 0x00FF00FFu) * 6553601u) >> 16;
+      const int adv_c = (int)(X & 0xffffu);
+      //   bases: (c|0x20) must equal "acgt"[h] with h = (lc>>1)&3 (v_perm table lookup)
+      const uint32_t lc = w0 | 0x20202020u;
+      const uint32_t hh = (lc >> 1) & 0x03030303u;
+      const uint32_t bad = lc ^ __builtin_amdgcn_perm(0u, 0x67746361u, hh);
+      const uint32_t codes = ((hh & 0x01010101u) << 1) | ((hh >> 1) & 0x01010101u);  // dict order A0 T1 C2 G3
+      const int shl = 8 * ((olen - 1) & 3);
+      const bool last_ok = ((bad >> shl) & 0xffu) == 0;  // '*': written base = operand[-1] (:96)
+      uint32_t pk = codes;
+      pk = (pk | (pk >> 6)) & 0x000f000fu;
+      pk = (pk | (pk >> 12)) & 0xffu;
+      uint32_t pay = star ? ((codes >> shl) & 3u) : (pk & ((1u << (2 * ol4)) - 1u));
+      bool slow = v & ((ex == (int)kNoEnd) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4)))));
+      int kind = !act ? 0 : colon ? (adv_c > 0 ? 1 : 0) : (olen <= 0) ? 0 : star ? 2 : plus ? 3 : minus ? 4 : 0;
+      int adv = kind == 1 ? adv_c : kind == 2 ? 1 : kind == 4 ? (olen < kAdvCap ? olen : kAdvCap) : 0;
+      uint32_t err = (v & !spec) ? DE_OP : 0u;  // cs does not start with an operator (:100-102)
+      if (act & star & (olen == 0)) err |= DE_INDEX;  // operand[-1] of '' (:96)
+      if ((kind == 2) & !last_ok) err |= DE_KEY;
+      if ((kind == 3) & ((bad & vm) != 0)) err |= DE_KEY;
       if (slow) {  // rare: decode from HBM
         const int64_t s = A + sx;
         int64_t e = A + ex;
@@ -552,10 +553,13 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       if (ins_inline)
         W.ibuf[nib + lanes_below(bins)] = te == 0 ? ins_event(itok, olen, pay, a.read_offset + rl)
                                                  : ins_event((int)kNullGap, 1, 0u, a.read_offset + rl);
+      bool rflank = false;
+      int ie = 0;
       if (last) {  // the read's last operation: i_end, downstream check, span
         const int64_t ia = i64 + adv;
-        const int ie = (int)(ia < 0 ? 0 : (ia > n ? n + 1 : ia));
+        ie = (int)(ia < 0 ? 0 : (ia > n ? n + 1 : ia));
         const int dnf = W.s_iend[q] & (1 << 30);
+        rflank = dnf && ie <= n;  // downstream flank = RIGHT event at gap i_end
         if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
         W.s_iend[q] = ie | dnf;
         const int ts = W.s_ts[q];
@@ -566,6 +570,12 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       G += atot;
       qc += __popcll(brs);
       nib += __popcll(bins);
+      const uint64_t brf = ballot(rflank);
+      if (brf) {
+        if (nib + 64 > kIB) flush_ibuf();
+        if (rflank) W.ibuf[nib + lanes_below(brf)] = flank_event(ie, true, a.read_offset + rl);
+        nib += __popcll(brf);
+      }
     }
     wave_sync_lds();
     // ---- reads that ended in this window: i_end; carry the open one ----
@@ -614,28 +624,31 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
     if (g0 & 31) atomicOr(a.hasleft + (g0 >> 5) + 1, v >> (32 - (g0 & 31)));
   }
   __syncthreads();
-  // ---- bucket-sort this workgroup's insertion events by gap (counting sort) ----
+  // ---- bucket-sort this workgroup's events by gap (counting sort): insertion
+  //      buckets [0, nbk), flank buckets [nbk, 2 nbk) ----
   const int nbk = (n + 1 + kBW - 1) / kBW;
+  const int nbt = 2 * nbk;
   uint32_t* bcnt = reinterpret_cast<uint32_t*>(uni);  // aliases the (flushed) tallies
-  uint32_t* bcur = bcnt + nbk;
+  uint32_t* bcur = bcnt + nbt;
   const int Ev = (int)misc[0];
-  for (int k = threadIdx.x; k < nbk; k += blockDim.x) bcnt[k] = 0;
+  for (int k = threadIdx.x; k < nbt; k += blockDim.x) bcnt[k] = 0;
   __syncthreads();
   for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
-    const uint32_t gap = (uint32_t)(a.ins_raw[rb_wg + k] >> 10) & kNullGap;
-    if (gap <= (uint32_t)n) atomicAdd(bcnt + gap / kBW, 1u);
+    const uint64_t ev = a.ins_raw[rb_wg + k];
+    const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
+    if (gap <= (uint32_t)n) atomicAdd(bcnt + gap / kBW + ((ev & kFlankBit) ? nbk : 0), 1u);
   }
   __syncthreads();
   if (threadIdx.x < 64) {  // exclusive scan over buckets by one wave
     int carry_b = 0;
-    for (int c0 = 0; c0 < nbk; c0 += 64) {
+    for (int c0 = 0; c0 < nbt; c0 += 64) {
       const int k = c0 + l;
-      const int v = k < nbk ? (int)bcnt[k] : 0;
+      const int v = k < nbt ? (int)bcnt[k] : 0;
       const int inc = wave_scan_i32(v);
-      if (k < nbk) {
+      if (k < nbt) {
         bcur[k] = (uint32_t)(carry_b + inc - v);
-        a.bk_cnt[(int64_t)blockIdx.x * a.nbmax + k] = v;
-        a.bk_off[(int64_t)blockIdx.x * a.nbmax + k] = carry_b + inc - v;
+        a.bk_cnt[(int64_t)blockIdx.x * a.nbs + k] = v;
+        a.bk_off[(int64_t)blockIdx.x * a.nbs + k] = carry_b + inc - v;
       }
       carry_b += wave_last_i32(inc);
     }
@@ -645,7 +658,7 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
     const uint64_t ev = a.ins_raw[rb_wg + k];
     const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
-    if (gap <= (uint32_t)n) a.ins_sorted[rb_wg + atomicAdd(bcur + gap / kBW, 1u)] = ev;
+    if (gap <= (uint32_t)n) a.ins_sorted[rb_wg + atomicAdd(bcur + gap / kBW + ((ev & kFlankBit) ? nbk : 0), 1u)] = ev;
   }
 }
 
@@ -680,11 +693,16 @@ __global__ __launch_bounds__(256) void K_rsplit(Dev d, uint32_t sentinel) {
   peel_atomic_max(d.maxR, g < 0 ? 0 : g, len, in && g >= 0 && !mixed);
 }
 
-// right_start[g] = #mixed RIGHT events with gap < g
+// right_start[g] = #mixed RIGHT events with gap < g; rpos[local read] = its
+// position in the sorted list (so consumers need no search)
 __global__ __launch_bounds__(256) void K_rstart(Dev d) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   if (t <= d.G) d.right_start[t] = (int32_t)lower_bound_u32(d.keys_out, 0, d.Ng, (uint32_t)t);
   if (t == 0) d.status[MPC_ST_MIXED] = (uint32_t)lower_bound_u32(d.keys_out, 0, d.Ng, (uint32_t)d.G);
+  if (t < d.Ng && d.keys_out[t] < (uint32_t)d.G) {
+    const int64_t lr = (int64_t)d.vals_out[t] - d.read_offset;
+    if (lr >= 0 && lr < d.N) d.rpos[lr] = (int32_t)t;
+  }
 }
 
 __global__ __launch_bounds__(256) void K_zero_runs(Dev d) {
@@ -709,19 +727,98 @@ __device__ __forceinline__ int64_t run_of2(const int32_t* right_start, const int
 }
 
 // ---------------------------------------------------------------------------
+// Bucketed event work units.  K_parse leaves, per parse workgroup, its events
+// counting-sorted into buckets of 16 gaps (insertion buckets [0, nbk), flank
+// buckets [nbk, 2 nbk)).  Entries of the host table `bc` are (sample, bucket,
+// chunk of <= 256 parse workgroups); K_units cuts every entry's events into
+// units of <= kUnit events (hot gaps -- every full-length read starts at gap 0
+// and ends at gap n -- become many units) and appends them to one list.
+// ---------------------------------------------------------------------------
+constexpr int kUnit = 1024;  // events per work unit
+
+struct UnitArgs {
+  const int4* bc;  // {sample, bucket, pw0, pw1}
+  const int32_t* bk_cnt; int4* units; uint32_t* status;
+  int64_t n_bc, units_cap;
+  int32_t nbs;
+};
+
+// one wave per table entry
+__global__ __launch_bounds__(256) void K_units(UnitArgs a) {
+  const int l = lane();
+  const int64_t ent = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (ent >= a.n_bc) return;
+  const int4 bc = a.bc[ent];
+  int t = 0;
+  for (int pw = bc.z + l; pw < bc.w; pw += 64) t += a.bk_cnt[(int64_t)pw * a.nbs + bc.y];
+  t = wave_sum(t);
+  const int nu = (t + kUnit - 1) / kUnit;
+  if (nu == 0) return;
+  uint32_t u0 = 0;
+  if (l == 0) u0 = atomicAdd(&a.status[MPC_ST_UNITS], (uint32_t)nu);
+  u0 = (uint32_t)__shfl((int)u0, 0, 64);
+  if ((int64_t)u0 + nu > a.units_cap) {
+    if (l == 0) atomicOr(&a.status[MPC_ST_FLAGS], DE_INTERNAL);
+    return;
+  }
+  for (int i = l; i < nu; i += 64) {
+    const int e0 = i * kUnit;
+    a.units[u0 + i] = make_int4((int)ent, e0, t - e0 < kUnit ? t - e0 : kUnit, 0);
+  }
+}
+
+// Per unit: the entry's <= 256 slices (counts, sources) lane-parallel, block
+// scan; afterwards event e of the entry is ins_sorted[s_src[j] + e - s_pre[j]]
+// with j = the last slice whose s_pre <= e.
+struct UnitView { int smp, bucket, e0, cnt; };
+__device__ __forceinline__ UnitView load_unit(const int4* bc_tab, const int4* units, int64_t u,
+                                              const int32_t* bk_cnt, const int32_t* bk_off, const int64_t* rbase,
+                                              int nbs, int32_t* s_pre, int64_t* s_src, int32_t* s_wsum) {
+  const int4 un = units[u];
+  const int4 bc = bc_tab[un.x];
+  const int l = lane(), w = threadIdx.x >> 6;
+  const int pw = bc.z + (int)threadIdx.x;
+  int cnt = 0;
+  int64_t src = 0;
+  if (pw < bc.w) {
+    const int64_t slot = (int64_t)pw * nbs + bc.y;
+    cnt = bk_cnt[slot];
+    src = rbase[pw] + bk_off[slot];
+  }
+  const int inc = wave_scan_i32(cnt);
+  if (l == 63) s_wsum[w] = inc;
+  __syncthreads();
+  int wpre = 0;
+  for (int k = 0; k < w; ++k) wpre += s_wsum[k];
+  s_pre[threadIdx.x] = wpre + inc - cnt;
+  s_src[threadIdx.x] = src;
+  __syncthreads();
+  return UnitView{bc.x, bc.y, un.y, un.z};
+}
+__device__ __forceinline__ int64_t unit_event_src(const int32_t* s_pre, const int64_t* s_src, int e) {
+  int lo = 0, hi = 255;  // last slice j with s_pre[j] <= e
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (s_pre[mid] <= e) lo = mid; else hi = mid - 1;
+  }
+  return s_src[lo] + (e - s_pre[lo]);
+}
+
+// ---------------------------------------------------------------------------
 // K_left: LEFT events -> per-run max length M and right-justified insertion
-// tallies F.  One workgroup per (sample, 16-gap bucket): it reads the bucket's
-// slice of every parse workgroup's bucket-sorted insertion events, so each gap
-// is owned by exactly one workgroup and its (gap, run) counters live in LDS
-// (runs k < kKMax; rarer runs go to HBM).  Upstream flank lengths and long
-// insertions only update M (grid-stride tails, wave-aggregated atomics).
+// tallies F.  Persistent workgroups over the work units: a unit's events all
+// lie in one 16-gap bucket, so its (gap, run) counters live in LDS (runs
+// k < kKMax; rarer runs go to HBM) and are flushed with atomics (several units
+// may share a bucket).  Upstream flanks are LEFT events too: their length
+// feeds M.  Long insertions (grid-stride tail) only update M.
 // ---------------------------------------------------------------------------
 struct LeftArgs {
-  const int64_t* up_off; const int32_t* tstart; const int32_t* sample;
-  const int32_t* n_of; const int32_t* gbase; const int4* work;  // {sample, bucket, pw0, pw1}
+  const int64_t* up_off; const int32_t* sample;
+  const int32_t* n_of; const int32_t* gbase;
+  const int4* bc; const int4* units; const uint32_t* status;
   const uint64_t* ins_sorted; const int32_t* bk_cnt; const int32_t* bk_off; const int64_t* rbase;
   int64_t N, read_offset, ovf_cap;
-  int32_t nbmax;
+  int32_t nbs;
   const int32_t* right_start; const int32_t* vals_out;
   int32_t* M; uint32_t* F;
   const Ovf* ovf; const uint32_t* ovf_cnt;
@@ -730,81 +827,84 @@ struct LeftArgs {
 __global__ __launch_bounds__(256) void K_left(LeftArgs a) {
   __shared__ uint32_t Fl[kBW][kKMax][16];
   __shared__ uint32_t Ml[kBW][kKMax];
-  const int l = lane();
-  const int w = uniform_i32((int)(threadIdx.x >> 6));
-  const int4 wk = a.work[blockIdx.x];
-  const int smp = wk.x, bk = wk.y, pw0 = wk.z, pw1 = wk.w;
-  const int n = a.n_of[smp];
-  const int gb = a.gbase[smp];
-  const int g0 = bk * kBW;
-  for (int k = threadIdx.x; k < kBW * kKMax * 16; k += blockDim.x) (&Fl[0][0][0])[k] = 0;
-  for (int k = threadIdx.x; k < kBW * kKMax; k += blockDim.x) (&Ml[0][0])[k] = 0;
-  __syncthreads();
-  for (int pw = pw0 + w; pw < pw1; pw += 4) {
-    const int64_t slot = (int64_t)pw * a.nbmax + bk;
-    const int cnt = a.bk_cnt[slot];
-    const int64_t src = a.rbase[pw] + a.bk_off[slot];
-    for (int e = l; e < cnt; e += 64) {
-      const uint64_t ev = a.ins_sorted[src + e];
+  __shared__ int32_t s_pre[256];
+  __shared__ int64_t s_src[256];
+  __shared__ int32_t s_wsum[4];
+  __shared__ int32_t s_rs[kBW + 1];  // right_start of the bucket's gaps
+  // (K_units raises DE_INTERNAL instead of overrunning the unit list)
+  const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
+  for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+    for (int k = threadIdx.x; k < kBW * kKMax * 16; k += blockDim.x) (&Fl[0][0][0])[k] = 0;
+    for (int k = threadIdx.x; k < kBW * kKMax; k += blockDim.x) (&Ml[0][0])[k] = 0;
+    {
+      const int4 bc = a.bc[a.units[u].x];
+      const int nn = a.n_of[bc.x];
+      const int nbk0 = (nn + 1 + kBW - 1) / kBW;
+      const int gg0 = (bc.y >= nbk0 ? bc.y - nbk0 : bc.y) * kBW;
+      const int gl = gg0 + kBW - 1 < nn ? gg0 + kBW - 1 : nn;
+      if ((int)threadIdx.x <= gl + 1 - gg0) s_rs[threadIdx.x] = a.right_start[a.gbase[bc.x] + gg0 + threadIdx.x];
+    }
+    const UnitView uv = load_unit(a.bc, a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, s_pre, s_src, s_wsum);
+    const int n = a.n_of[uv.smp];
+    const int gb = a.gbase[uv.smp];
+    const int nbk = (n + 1 + kBW - 1) / kBW;
+    const int g0 = (uv.bucket >= nbk ? uv.bucket - nbk : uv.bucket) * kBW;
+    for (int e = uv.e0 + (int)threadIdx.x; e < uv.e0 + uv.cnt; e += blockDim.x) {
+      const uint64_t ev = a.ins_sorted[unit_event_src(s_pre, s_src, e)];
       const int gap = (int)((ev >> 10) & kNullGap);
       if (gap > n || gap < g0 || gap >= g0 + kBW) continue;
-      const int L = (int)((ev >> 8) & 3u) + 1;
-      const int64_t rg = (int64_t)(ev >> 32);
       const int64_t g = (int64_t)gb + gap;
-      const int64_t run = run_of2(a.right_start, a.vals_out, g, rg);
-      const int64_t k = run - (a.right_start[g] + g);
+      const int64_t rg = event_read(ev);
+      int L;
+      if (ev & kFlankBit) {
+        if (ev & kDownBit) continue;  // downstream flanks: RIGHT events (K_rsplit / K_seg_right)
+        const int64_t r = rg - a.read_offset;
+        const int64_t uln = a.up_off[r + 1] - a.up_off[r];
+        L = uln > 0x7fffffff ? 0x7fffffff : (int)uln;
+      } else {
+        L = (int)((ev >> 8) & 3u) + 1;
+      }
+      const int32_t ra = s_rs[gap - g0], rb = s_rs[gap - g0 + 1];
+      const int64_t k = rb > ra ? lower_bound_i32(a.vals_out, ra, rb, (int32_t)rg) - ra : 0;
+      const int64_t run = ra + g + k;
+      const bool ins = !(ev & kFlankBit);
       if (k < kKMax) {
         atomicMax(&Ml[gap - g0][k], (uint32_t)L);
-        for (int bi = 0; bi < L; ++bi) {  // bi counts from the 3' end (:55-61)
-          const int code = (int)((ev >> (2 * (L - 1 - bi))) & 3u);
-          atomicAdd(&Fl[gap - g0][k][bi * 4 + code], 1u);
-        }
+        if (ins)
+          for (int bi = 0; bi < L; ++bi) {  // bi counts from the 3' end (:55-61)
+            const int code = (int)((ev >> (2 * (L - 1 - bi))) & 3u);
+            atomicAdd(&Fl[gap - g0][k][bi * 4 + code], 1u);
+          }
       } else {
         atomicMax(a.M + run, L);
-        for (int bi = 0; bi < L; ++bi) {
-          const int code = (int)((ev >> (2 * (L - 1 - bi))) & 3u);
-          atomicAdd(a.F + run * 16 + bi * 4 + code, 1u);
-        }
+        if (ins)
+          for (int bi = 0; bi < L; ++bi) {
+            const int code = (int)((ev >> (2 * (L - 1 - bi))) & 3u);
+            atomicAdd(a.F + run * 16 + bi * 4 + code, 1u);
+          }
       }
     }
-  }
-  // upstream flanks: LEFT event at gap tstart contributes its length to M
-  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < a.N; r0 += nthreads) {
-    const int64_t r = r0 + threadIdx.x;
-    bool act = false;
-    int64_t run = 0;
-    int32_t ul = 0;
-    if (r < a.N) {
-      const int s = a.sample[r];
-      const int ts = a.tstart[r];
-      const int64_t u = a.up_off[r + 1] - a.up_off[r];
-      ul = u > 0x7fffffff ? 0x7fffffff : (int32_t)u;
-      if (ul > 0 && ts >= 0 && ts <= a.n_of[s]) {
-        act = true;
-        run = run_of2(a.right_start, a.vals_out, (int64_t)a.gbase[s] + ts, a.read_offset + r);
-      }
+    __syncthreads();
+    // flush: lanes sweep (gap, run, field) so each 16-field row is contiguous
+    for (int q = threadIdx.x; q < kBW * kKMax * 16; q += blockDim.x) {
+      const int f = q & 15, k = (q >> 4) % kKMax, p = q / (16 * kKMax);
+      const uint32_t m = Ml[p][k];
+      if (!m) continue;
+      const int64_t g = (int64_t)gb + g0 + p;
+      const int64_t run = s_rs[p] + g + k;
+      if (f == 0) atomicMax(a.M + run, (int32_t)m);
+      const uint32_t v = Fl[p][k][f];
+      if (v) atomicAdd(a.F + run * 16 + f, v);
     }
-    peel_atomic_max(a.M, run, ul, act);
+    __syncthreads();
   }
   // long insertions
+  const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
   const int64_t nov = *a.ovf_cnt < (uint32_t)a.ovf_cap ? *a.ovf_cnt : a.ovf_cap;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nov; t += nthreads) {
     const Ovf o = a.ovf[t];
     const int64_t g = (int64_t)a.gbase[a.sample[o.read]] + o.gap;
     atomicMax(a.M + run_of2(a.right_start, a.vals_out, g, a.read_offset + o.read), o.len);
-  }
-  __syncthreads();
-  // flush: lanes sweep (gap, run, field) so each 16-field row is contiguous
-  for (int q = threadIdx.x; q < kBW * kKMax * 16; q += blockDim.x) {
-    const int f = q & 15, k = (q >> 4) % kKMax, p = q / (16 * kKMax);
-    const uint32_t m = Ml[p][k];
-    if (!m) continue;
-    const int64_t g = (int64_t)gb + g0 + p;
-    const int64_t run = a.right_start[g] + g + k;
-    if (f == 0) atomicMax(a.M + run, (int32_t)m);
-    const uint32_t v = Fl[p][k][f];
-    if (v) atomicAdd(a.F + run * 16 + f, v);
   }
 }
 
@@ -950,158 +1050,182 @@ __global__ __launch_bounds__(256) void K_assemble(Dev d) {
   }
 }
 
-// Flank / long-insertion tallies.  Hot rows (every full-length read's upstream
-// flank lands on gap 0, every downstream flank on gap n) are aggregated in an
-// LDS open-addressed table keyed by row, then flushed with global atomics.
-constexpr int kHash = 2048;
-constexpr uint32_t kEmpty = 0xffffffffu;
+// ---------------------------------------------------------------------------
+// Flank tallies (:37-72 applied to the flank strings).  Every flank base lands
+// in the slot block of its anchor gap, so a workgroup owns one 16-gap bucket
+// (and a chunk of the parse workgroups whose bucketed flank events it reads):
+// it tallies the bucket's row range in a dense LDS histogram, bytes processed
+// flat across events, then flushes with global atomics (hot buckets are split
+// over several workgroups).  A grid-stride tail adds the long insertions.
+// ---------------------------------------------------------------------------
+constexpr int kFlankRows = 2048;  // dense LDS rows per unit (else HBM atomics)
 
-__device__ __forceinline__ void hash_add(uint32_t* keys, uint32_t* vals, uint32_t* rows, uint32_t row, int code) {
-  uint32_t h = (row * 2654435761u) & (kHash - 1);
-#pragma unroll 1
-  for (int probe = 0; probe < 32; ++probe) {
-    const uint32_t k = keys[h];
-    if (k == row) { atomicAdd(vals + h * 4 + code, 1u); return; }
-    if (k == kEmpty) {
-      const uint32_t prev = atomicCAS(keys + h, kEmpty, row);
-      if (prev == kEmpty || prev == row) { atomicAdd(vals + h * 4 + code, 1u); return; }
-    }
-    h = (h + 1) & (kHash - 1);
-  }
-  atomicAdd(rows + (uint64_t)row * 4 + code, 1u);  // table full: go straight to HBM
-}
-
-struct StrArgs {
+struct FlankArgs {
   uint32_t* status; const int32_t* sample; const int32_t* n_of; const int32_t* gbase;
+  const int4* bc; const int4* units;
+  const uint64_t* ins_sorted; const int32_t* bk_cnt; const int32_t* bk_off; const int64_t* rbase;
   int64_t N, read_offset, ovf_cap;
-  const int64_t* up_off; const uint8_t* up; const int32_t* tstart;
-  const int64_t* down_off; const uint8_t* down; const int32_t* i_end;
-  const int32_t* right_start; const int32_t* vals_out; const int32_t* row_base; const int32_t* lo_f;
-  const int32_t* seg_hi; const int32_t* seg_lo; const int32_t* hscan;
+  int32_t nbs;
+  const int64_t* up_off; const uint8_t* up; const int64_t* down_off; const uint8_t* down;
+  const int32_t* right_start; const int32_t* vals_out; const int32_t* row_base; const int32_t* rowcnt;
+  const int32_t* lo_f; const int32_t* seg_hi; const int32_t* seg_lo; const int32_t* hscan; const int32_t* rpos;
   uint32_t* rows; const Ovf* ovf; const uint32_t* ovf_cnt; const uint8_t* cs;
 };
 
-// One wave takes 64 consecutive reads: lane j resolves read j's two flank
-// anchors (row of base 0 and direction).  Because the reads are consecutive,
-// their upstream (downstream) flanks form ONE contiguous byte range; the wave
-// streams that range with coalesced 4-byte loads and maps each byte back to
-// its read by a short search over the 64 offsets held in LDS.
-__device__ __forceinline__ void strings_range(const StrArgs& d, const uint8_t* bytes, int64_t x0, int64_t x1,
-                                              const int64_t* off, const int64_t* anc, bool left, int nb,
-                                              uint32_t* keys, uint32_t* vals, uint32_t& lerr, int64_t& lread,
-                                              int64_t base) {
-  const int l = lane();
-  const int64_t a0 = x0 & ~(int64_t)3;
-  for (int64_t w0 = a0; w0 < x1; w0 += 256) {
-    const int64_t wx = w0 + 4 * l;
-    uint32_t word = 0;
-    if (wx < x1) word = *reinterpret_cast<const uint32_t*>(bytes + wx);
-    if (wx + 4 <= x0 || wx >= x1) continue;
-    // read containing byte wx (or the first byte >= x0): last j with off[j] <= max(wx, x0)
-    const int64_t first = wx < x0 ? x0 : wx;
-    int lo = 0, hi = nb - 1;
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (off[mid] <= first) lo = mid; else hi = mid - 1;
-    }
-#pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      const int64_t x = wx + k;
-      if (x < x0 || x >= x1) continue;
-      while (lo + 1 < nb && off[lo + 1] <= x) ++lo;
-      const int64_t ank = anc[lo];
-      if (ank == INT64_MIN) continue;  // this read's flank is not placed (beyond the reference end)
-      const int code = base_code_exact((word >> (8 * k)) & 0xffu);
-      if (code < 0) { lerr |= DE_KEY; lread = base + lo; continue; }
-      // LEFT: base bi counted from the 3' end sits at anchor - bi, bi = end-1-x ;
-      // RIGHT: base bi = x - start sits at anchor + bi
-      const int64_t row = left ? ank - (off[lo + 1] - 1 - x) : ank + (x - off[lo]);
-      hash_add(keys, vals, d.rows, (uint32_t)row, code);
-    }
-  }
-}
-
-__global__ __launch_bounds__(256) void K_strings(StrArgs d) {
-  __shared__ uint32_t s_keys[kHash];
-  __shared__ uint32_t s_vals[kHash * 4];
-  __shared__ int64_t s_uoff[4][65], s_doff[4][65], s_uanc[4][64], s_danc[4][64];
-  if (d.status[MPC_ST_FLAGS] & DE_CAP) return;
-  for (int k = threadIdx.x; k < kHash; k += blockDim.x) s_keys[k] = kEmpty;
-  for (int k = threadIdx.x; k < kHash * 4; k += blockDim.x) s_vals[k] = 0;
-  __syncthreads();
+__global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
+  __shared__ uint32_t cnt[kFlankRows * 4];
+  __shared__ int32_t s_pre[256];
+  __shared__ int64_t s_src[256];
+  __shared__ int32_t s_wsum[4];
+  __shared__ int64_t e_off[256], e_anc[256];
+  __shared__ int32_t e_pre[256], e_len[256];
+  __shared__ int32_t e_read[256];
+  __shared__ uint8_t e_down[256];
+  // per gap of the bucket: sorted-RIGHT range, row base, lo, hi of run 0
+  __shared__ int32_t s_rs[kBW + 1], s_rowb[kBW], s_lof[kBW], s_hi0[kBW];
   const int l = lane();
   const int w = uniform_i32((int)(threadIdx.x >> 6));
+  const int tid = threadIdx.x;
+  if (a.status[MPC_ST_FLAGS] & DE_CAP) return;
   uint32_t lerr = 0;
   int64_t lread = -1;
-  const int64_t nbatch = (d.N + 63) / 64;
-  for (int64_t bt = (int64_t)blockIdx.x * 4 + w; bt < nbatch; bt += (int64_t)gridDim.x * 4) {
-    const int64_t base = bt * 64;
-    const int nb = (int)(d.N - base < 64 ? d.N - base : 64);
-    int64_t uanc = INT64_MIN, danc = INT64_MIN;
-    if (l < nb) {
-      const int64_t r = base + l;
-      const int s = d.sample[r];
-      const int64_t n = d.n_of[s];
-      const int64_t gb = d.gbase[s];
-      const int64_t rg = d.read_offset + r;
-      const int64_t ts = d.tstart[r];
-      const int64_t ie = d.i_end[r];
-      s_uoff[w][l] = d.up_off[r];
-      s_doff[w][l] = d.down_off[r];
-      if (l == nb - 1) { s_uoff[w][nb] = d.up_off[r + 1]; s_doff[w][nb] = d.down_off[r + 1]; }
-      if (ts >= 0 && ts <= n) {            // LEFT at gap tstart: row = lo + hi_run - 1 - bi
-        const int64_t g = gb + ts;
-        const int64_t run = run_of2(d.right_start, d.vals_out, g, rg);
-        uanc = (int64_t)d.row_base[g] + d.lo_f[g] + d.seg_hi[d.hscan[run] - 1] - 1;
-      }
-      if (ie <= n) {                       // RIGHT at gap i_end: row = lo - lo_at + bi
-        const int64_t g = gb + ie;
-        int64_t lo_at = 0;
-        const int64_t a = d.right_start[g], b = d.right_start[g + 1];
-        if (b > a) {                       // mixed gap: this read's RIGHT event
-          const int64_t t = lower_bound_i32(d.vals_out, a, b, (int32_t)rg);
-          lo_at = d.seg_lo[d.hscan[t + g] - 1];
-        }
-        danc = (int64_t)d.row_base[g] + d.lo_f[g] - lo_at;
+  // (K_units raises DE_INTERNAL instead of overrunning the unit list)
+  const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
+  for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+    {  // flank units only
+      const int4 bc = a.bc[a.units[u].x];
+      const int nn = a.n_of[bc.x];
+      const int nbk0 = (nn + 1 + kBW - 1) / kBW;
+      if (bc.y < nbk0) continue;
+      const int gg0 = (bc.y - nbk0) * kBW;
+      const int gl = gg0 + kBW - 1 < nn ? gg0 + kBW - 1 : nn;
+      const int64_t gbb = a.gbase[bc.x];
+      if (tid <= gl + 1 - gg0) s_rs[tid] = a.right_start[gbb + gg0 + tid];
+      if (tid <= gl - gg0) {
+        const int64_t g = gbb + gg0 + tid;
+        s_rowb[tid] = a.row_base[g];
+        s_lof[tid] = a.lo_f[g];
+        s_hi0[tid] = a.seg_hi[a.hscan[a.right_start[g] + g] - 1];
       }
     }
-    s_uanc[w][l] = uanc;
-    s_danc[w][l] = danc;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    strings_range(d, d.up, s_uoff[w][0], s_uoff[w][nb], s_uoff[w], s_uanc[w], true, nb, s_keys, s_vals, lerr,
-                  lread, base);
-    strings_range(d, d.down, s_doff[w][0], s_doff[w][nb], s_doff[w], s_danc[w], false, nb, s_keys, s_vals, lerr,
-                  lread, base);
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const UnitView uv = load_unit(a.bc, a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, s_pre, s_src, s_wsum);
+    const int n = a.n_of[uv.smp];
+    const int64_t gb = a.gbase[uv.smp];
+    const int nbk = (n + 1 + kBW - 1) / kBW;
+    const int g0 = (uv.bucket - nbk) * kBW;
+    const int gl = (g0 + kBW - 1 < n ? g0 + kBW - 1 : n);  // last gap of the bucket
+    const int64_t R0 = s_rowb[0];
+    const int64_t R1 = (int64_t)s_rowb[gl - g0] + a.rowcnt[gb + gl];
+    const bool dense = R1 - R0 <= kFlankRows;
+    if (dense)
+      for (int k = tid; k < (int)(R1 - R0) * 4; k += blockDim.x) cnt[k] = 0;
+    for (int e0 = uv.e0; e0 < uv.e0 + uv.cnt; e0 += 256) {
+      // one event per thread: anchor row and flank byte range
+      const int e = e0 + tid;
+      int len = 0;
+      int64_t off = 0, anc = 0;
+      bool down = false;
+      int64_t r = 0;
+      if (e < uv.e0 + uv.cnt) {
+        const uint64_t ev = a.ins_sorted[unit_event_src(s_pre, s_src, e)];
+        const int gap = (int)((ev >> 10) & kNullGap);
+        const int p = gap - g0;
+        const int64_t rg = event_read(ev);
+        r = rg - a.read_offset;
+        down = (ev & kDownBit) != 0;
+        const int64_t g = gb + gap;
+        const int32_t ra = s_rs[p], rb = s_rs[p + 1];
+        int64_t L;
+        if (!down) {  // LEFT at gap tstart: base bi (from the 3' end) -> row lo + hi_run - 1 - bi
+          int32_t hi = s_hi0[p];
+          if (rb > ra) {  // mixed gap: run k = RIGHT events of earlier reads
+            const int64_t k = lower_bound_i32(a.vals_out, ra, rb, (int32_t)rg) - ra;
+            hi = a.seg_hi[a.hscan[ra + g + k] - 1];
+          }
+          anc = (int64_t)s_rowb[p] + s_lof[p] + hi - 1;
+          off = a.up_off[r];
+          L = a.up_off[r + 1] - off;
+        } else {      // RIGHT at gap i_end: base bi -> row lo - lo_at + bi
+          int64_t lo_at = 0;
+          bool ok = true;
+          if (rb > ra) {  // mixed gap: this read's RIGHT event in the sorted list
+            const int64_t t = a.rpos[r];
+            ok = t >= ra && t < rb;
+            if (ok) lo_at = a.seg_lo[a.hscan[t + g] - 1];
+            else lerr |= DE_INTERNAL;
+          }
+          anc = (int64_t)s_rowb[p] + s_lof[p] - lo_at;
+          off = a.down_off[r];
+          L = ok ? a.down_off[r + 1] - off : 0;
+        }
+        len = L > (1 << 30) ? (1 << 30) : (int)L;
+      }
+      const int nch = (len + 3) >> 2;  // 4-byte chunks of this flank
+      {  // block scan of chunk counts
+        const int inc = wave_scan_i32(nch);
+        __syncthreads();
+        if (l == 63) s_wsum[w] = inc;
+        __syncthreads();
+        int wpre = 0;
+        for (int k = 0; k < w; ++k) wpre += s_wsum[k];
+        e_pre[tid] = wpre + inc - nch;
+        e_len[tid] = len;
+        e_off[tid] = off;
+        e_anc[tid] = anc;
+        e_read[tid] = (int32_t)r;
+        e_down[tid] = down ? 1 : 0;
+      }
+      const int nchunks = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
+      __syncthreads();
+      for (int x = tid; x < nchunks; x += blockDim.x) {
+        int lo = 0, hi = 255;  // last event j with e_pre[j] <= x
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (e_pre[mid] <= x) lo = mid; else hi = mid - 1;
+        }
+        const int b0 = 4 * (x - e_pre[lo]);
+        const int L = e_len[lo];
+        const bool dn = e_down[lo] != 0;
+        const uint8_t* src8 = (dn ? a.down : a.up) + e_off[lo];
+        uint32_t c4[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) c4[k] = b0 + k < L ? src8[b0 + k] : 0u;
+        const int64_t anc = e_anc[lo];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int bi = b0 + k;
+          if (bi >= L) break;
+          const int code = base_code_exact(c4[k]);
+          if (code < 0) { lerr |= DE_KEY; lread = e_read[lo]; continue; }  // flank base not in the dict (:61, :71)
+          const int64_t row = dn ? anc + bi : anc - (L - 1 - bi);
+          if (dense && row >= R0 && row < R1) atomicAdd(cnt + (row - R0) * 4 + code, 1u);
+          else atomicAdd(a.rows + row * 4 + code, 1u);
+        }
+      }
+      __syncthreads();
+    }
+    if (dense)
+      for (int k = tid; k < (int)(R1 - R0) * 4; k += blockDim.x) {
+        const uint32_t v = cnt[k];
+        if (v) atomicAdd(a.rows + R0 * 4 + k, v);
+      }
+    __syncthreads();
   }
   // long insertions (grid-stride, LEFT like the short ones)
-  const int64_t nov = *d.ovf_cnt < (uint32_t)d.ovf_cap ? *d.ovf_cnt : d.ovf_cap;
-  for (int64_t t = blockIdx.x * 4 + w; t < nov; t += (int64_t)gridDim.x * 4) {
-    const Ovf o = d.ovf[t];
-    const int64_t g = d.gbase[d.sample[o.read]] + o.gap;
-    const int64_t run = run_of2(d.right_start, d.vals_out, g, d.read_offset + o.read);
-    const int64_t rb = (int64_t)d.row_base[g] + d.lo_f[g] + d.seg_hi[d.hscan[run] - 1] - 1;
+  const int64_t nov = *a.ovf_cnt < (uint32_t)a.ovf_cap ? *a.ovf_cnt : a.ovf_cap;
+  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < nov; t += (int64_t)gridDim.x * 4) {
+    const Ovf o = a.ovf[t];
+    const int64_t g = a.gbase[a.sample[o.read]] + o.gap;
+    const int64_t run = run_of2(a.right_start, a.vals_out, g, a.read_offset + o.read);
+    const int64_t rb = (int64_t)a.row_base[g] + a.lo_f[g] + a.seg_hi[a.hscan[run] - 1] - 1;
     for (int64_t bi = l; bi < o.len; bi += 64) {
-      const int c = code_upper(d.cs[o.off + o.len - 1 - bi]);
-      hash_add(s_keys, s_vals, d.rows, (uint32_t)(rb - bi), c < 0 ? 0 : c);
+      const int c = code_upper(a.cs[o.off + o.len - 1 - bi]);
+      atomicAdd(a.rows + (rb - bi) * 4 + (c < 0 ? 0 : c), 1u);
     }
   }
   if (lerr) {
-    atomicOr(&d.status[MPC_ST_FLAGS], lerr);
-    atomicMin(&d.status[MPC_ST_FIRST_READ], (uint32_t)lread);
-  }
-  __syncthreads();
-  for (int k = threadIdx.x; k < kHash; k += blockDim.x) {
-    const uint32_t row = s_keys[k];
-    if (row == kEmpty) continue;
-    for (int c = 0; c < 4; ++c) {
-      const uint32_t v = s_vals[k * 4 + c];
-      if (v) atomicAdd(d.rows + (uint64_t)row * 4 + c, v);
-    }
+    atomicOr(&a.status[MPC_ST_FLAGS], lerr);
+    if (lread >= 0) atomicMin(&a.status[MPC_ST_FIRST_READ], (uint32_t)lread);
   }
 }
 
@@ -1221,14 +1345,15 @@ struct mpc_plan {
   size_t ws_bytes = 0;
   uint8_t* ws = nullptr;
   size_t cub_tmp = 0;
-  std::vector<int32_t> work_parse, work_left;  // int4 records
-  int n_parse_wg = 0, n_left_wg = 0, parse_lds = 0, nbmax = 1;
+  std::vector<int32_t> work_parse, work_bc;  // int4 records
+  int n_parse_wg = 0, parse_lds = 0, nbmax = 1;
+  int64_t n_bc = 0, units_cap = 0;
   bool fused = false;
   enum {
     B_STATUS, B_NOF, B_GBASE, B_IEND, B_INSRAW, B_INSSORT, B_BKCNT, B_BKOFF, B_RBASE, B_OVF, B_OVFCNT,
-    B_HASLEFT, B_MAXR, B_KIN, B_VIN, B_KOUT, B_VOUT, B_RLEN, B_RSTART, B_DIFF, B_SUB, B_M, B_F,
+    B_HASLEFT, B_MAXR, B_KIN, B_VIN, B_KOUT, B_VOUT, B_RLEN, B_RPOS, B_RSTART, B_DIFF, B_SUB, B_M, B_F,
     B_HFLAG, B_HSCAN, B_SEGR, B_SEGLO, B_SEGHI, B_SEGRUN, B_LOF, B_ROWCNT, B_ROWBASE, B_DEPTH, B_ROWS,
-    B_META, B_RES, B_KEEP, B_KEEPSCAN, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WLEFT, B_CUB, B_COUNT
+    B_META, B_RES, B_KEEP, B_KEEPSCAN, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_CUB, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -1251,7 +1376,7 @@ Dev mpc_plan::dev() const {
   d.hasleft = at<uint32_t>(this, B_HASLEFT); d.maxR = at<int32_t>(this, B_MAXR);
   d.keys_in = at<uint32_t>(this, B_KIN); d.vals_in = at<int32_t>(this, B_VIN);
   d.keys_out = at<uint32_t>(this, B_KOUT); d.vals_out = at<int32_t>(this, B_VOUT);
-  d.rlen = at<int32_t>(this, B_RLEN); d.right_start = at<int32_t>(this, B_RSTART);
+  d.rlen = at<int32_t>(this, B_RLEN); d.rpos = at<int32_t>(this, B_RPOS); d.right_start = at<int32_t>(this, B_RSTART);
   d.diff = at<int32_t>(this, B_DIFF); d.sub = at<uint32_t>(this, B_SUB);
   d.M = at<int32_t>(this, B_M); d.F = at<uint32_t>(this, B_F);
   d.hflag = at<int32_t>(this, B_HFLAG); d.hscan = at<int32_t>(this, B_HSCAN);
@@ -1271,7 +1396,7 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.n_of = d.n_of; a.gbase = d.gbase;
   a.work = reinterpret_cast<const int4*>(p->ws + p->off[mpc_plan::B_WPARSE]);
   a.cs_base = d.cs_base; a.ovf_cap = d.ovf_cap; a.read_offset = d.read_offset; a.n_reads = d.N;
-  a.fused = p->fused ? 1 : 0; a.nbmax = p->nbmax;
+  a.fused = p->fused ? 1 : 0; a.nbs = 2 * p->nbmax;
   a.i_end = d.i_end;
   a.ins_raw = at<uint64_t>(p, mpc_plan::B_INSRAW); a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
@@ -1290,24 +1415,39 @@ static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
 
 static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
   LeftArgs a;
-  a.up_off = d.up_off; a.tstart = d.tstart; a.sample = d.sample; a.n_of = d.n_of; a.gbase = d.gbase;
-  a.work = reinterpret_cast<const int4*>(p->ws + p->off[mpc_plan::B_WLEFT]);
+  a.up_off = d.up_off; a.sample = d.sample; a.n_of = d.n_of; a.gbase = d.gbase;
+  a.bc = at<const int4>(p, mpc_plan::B_WBC); a.units = at<const int4>(p, mpc_plan::B_UNITS); a.status = d.status;
   a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
   a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
-  a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbmax = p->nbmax;
+  a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = 2 * p->nbmax;
   a.right_start = d.right_start; a.vals_out = d.vals_out; a.M = d.M; a.F = d.F;
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt;
   return a;
 }
 
-static StrArgs str_args(const Dev& d) {
-  StrArgs a;
-  a.status = d.status; a.sample = d.sample; a.n_of = d.n_of; a.gbase = d.gbase; a.N = d.N;
-  a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.up_off = d.up_off; a.up = d.up; a.tstart = d.tstart;
-  a.down_off = d.down_off; a.down = d.down; a.i_end = d.i_end; a.right_start = d.right_start;
-  a.vals_out = d.vals_out; a.row_base = d.row_base; a.lo_f = d.lo_f; a.seg_hi = d.seg_hi; a.seg_lo = d.seg_lo;
-  a.hscan = d.hscan; a.rows = d.rows; a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.cs = d.cs;
+static UnitArgs unit_args(const mpc_plan* p, const Dev& d) {
+  UnitArgs a;
+  a.bc = at<const int4>(p, mpc_plan::B_WBC); a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT);
+  a.units = at<int4>(p, mpc_plan::B_UNITS); a.status = d.status;
+  a.n_bc = p->n_bc; a.units_cap = p->units_cap; a.nbs = 2 * p->nbmax;
+  return a;
+}
+static int64_t left_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 1024)); }
+static int64_t flank_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 768)); }
+
+static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
+  FlankArgs a;
+  a.status = d.status; a.sample = d.sample; a.n_of = d.n_of; a.gbase = d.gbase;
+  a.bc = at<const int4>(p, mpc_plan::B_WBC); a.units = at<const int4>(p, mpc_plan::B_UNITS);
+  a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
+  a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
+  a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
+  a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = 2 * p->nbmax;
+  a.up_off = d.up_off; a.up = d.up; a.down_off = d.down_off; a.down = d.down;
+  a.right_start = d.right_start; a.vals_out = d.vals_out; a.row_base = d.row_base; a.rowcnt = d.rowcnt;
+  a.lo_f = d.lo_f; a.seg_hi = d.seg_hi; a.seg_lo = d.seg_lo; a.hscan = d.hscan; a.rpos = d.rpos;
+  a.rows = d.rows; a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.cs = d.cs;
   return a;
 }
 
@@ -1316,10 +1456,6 @@ static inline unsigned nblk(int64_t n, int b = 256) {
   if (g < 1) g = 1;
   if (g > 65535 * 16) g = 65535 * 16;
   return (unsigned)g;
-}
-
-static unsigned strings_grid(int64_t N) {
-  return (unsigned)std::max<int64_t>(1, std::min<int64_t>((N + 255) / 256, 1024));
 }
 
 extern "C" {
@@ -1349,10 +1485,10 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   p->h_gbase[p->S] = (int32_t)g;
   p->G = g;
   if (p->G >= (1ll << 30)) { delete p; return fail(MPC_E_ARG, "too many positions"); }
-  if (p->Ng >= (1ll << 31) - 1) { delete p; return fail(MPC_E_ARG, "too many reads"); }
+  if (p->Ng >= (1ll << 30)) { delete p; return fail(MPC_E_ARG, "too many reads (event words hold 30-bit read indices)"); }
   p->row_cap = row_cap > 0 ? row_cap : 1;
   p->runs_cap = p->Ng + p->G;
-  p->ins_cap = in->cs_bytes / 2 + p->N + 16;
+  p->ins_cap = in->cs_bytes / 2 + 3 * p->N + 16;  // insertions + 2 flank events per read
   p->ovf_cap = in->cs_bytes / 6 + 16;
   int eb = 1;
   while ((1ll << eb) <= p->G + 1) ++eb;
@@ -1389,9 +1525,12 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     for (int s = 0; s < p->S; ++s) {
       const int nb = (int)((p->ref_len[s] + 1 + kBW - 1) / kBW);
       if (pw_begin[s + 1] == pw_begin[s]) continue;  // no reads: nothing to tally
-      for (int b = 0; b < nb; ++b) p->work_left.insert(p->work_left.end(), {s, b, pw_begin[s], pw_begin[s + 1]});
+      for (int b = 0; b < 2 * nb; ++b)  // insertion buckets, then flank buckets
+        for (int c = pw_begin[s]; c < pw_begin[s + 1]; c += 256)
+          p->work_bc.insert(p->work_bc.end(), {s, b, c, std::min(c + 256, pw_begin[s + 1])});
     }
-    p->n_left_wg = (int)(p->work_left.size() / 4);
+    p->n_bc = (int64_t)(p->work_bc.size() / 4);
+    p->units_cap = p->ins_cap / kUnit + p->n_bc + 1;
   }
   {
     size_t t = 0;
@@ -1416,8 +1555,8 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_IEND, N, 4);
   set(mpc_plan::B_INSRAW, p->ins_cap, 8);
   set(mpc_plan::B_INSSORT, p->ins_cap, 8);
-  set(mpc_plan::B_BKCNT, (int64_t)p->n_parse_wg * p->nbmax, 4);
-  set(mpc_plan::B_BKOFF, (int64_t)p->n_parse_wg * p->nbmax, 4);
+  set(mpc_plan::B_BKCNT, (int64_t)p->n_parse_wg * 2 * p->nbmax, 4);
+  set(mpc_plan::B_BKOFF, (int64_t)p->n_parse_wg * 2 * p->nbmax, 4);
   set(mpc_plan::B_RBASE, p->n_parse_wg, 8);
   set(mpc_plan::B_OVF, p->ovf_cap, sizeof(Ovf));
   set(mpc_plan::B_OVFCNT, 1, 4);
@@ -1428,6 +1567,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_KOUT, Ng, 4);
   set(mpc_plan::B_VOUT, Ng, 4);
   set(mpc_plan::B_RLEN, Ng, 4);
+  set(mpc_plan::B_RPOS, N > 0 ? N : 1, 4);
   set(mpc_plan::B_RSTART, G + 1, 4);
   set(mpc_plan::B_DIFF, G, 4);
   set(mpc_plan::B_SUB, G * 4, 4);
@@ -1452,7 +1592,8 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_NCALLS, p->S + 1, 4);
   set(mpc_plan::B_MAXD, p->S, 4);
   set(mpc_plan::B_WPARSE, (int64_t)p->work_parse.size(), 4);
-  set(mpc_plan::B_WLEFT, (int64_t)p->work_left.size(), 4);
+  set(mpc_plan::B_WBC, (int64_t)p->work_bc.size(), 4);
+  set(mpc_plan::B_UNITS, p->units_cap * 4, 4);
   set(mpc_plan::B_CUB, (int64_t)p->cub_tmp, 1);
   size_t o = 0;
   for (int b = 0; b < mpc_plan::B_COUNT; ++b) {
@@ -1491,8 +1632,8 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
   HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_GBASE), p->h_gbase.data(), 4 * (p->S + 1), hipMemcpyHostToDevice));
   if (!p->work_parse.empty())
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WPARSE), p->work_parse.data(), 4 * p->work_parse.size(), hipMemcpyHostToDevice));
-  if (!p->work_left.empty())
-    HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WLEFT), p->work_left.data(), 4 * p->work_left.size(), hipMemcpyHostToDevice));
+  if (!p->work_bc.empty())
+    HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WBC), p->work_bc.data(), 4 * p->work_bc.size(), hipMemcpyHostToDevice));
   HIPCHK(hipFuncSetAttribute((const void*)K_parse<true>, hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
   HIPCHK(hipFuncSetAttribute((const void*)K_parse<false>, hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
   p->bound = true;
@@ -1552,7 +1693,7 @@ int mpc_index(mpc_plan* p, void* stream) {
   } else {
     HIPCHK(hipMemsetAsync(d.keys_out, 0xff, 4, st));
   }
-  hipLaunchKernelGGL(K_rstart, dim3(nblk(p->G + 1)), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(K_rstart, dim3(nblk(std::max<int64_t>(p->G + 1, p->Ng))), dim3(256), 0, st, d);
   hipLaunchKernelGGL(K_zero_runs, dim3(nblk(p->runs_cap)), dim3(256), 0, st, d);
   HIPCHK(hipGetLastError());
   return MPC_OK;
@@ -1562,7 +1703,8 @@ int mpc_tally(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  if (p->n_left_wg > 0) hipLaunchKernelGGL(K_left, dim3(p->n_left_wg), dim3(256), 0, st, left_args(p, d));
+  if (p->n_bc > 0) hipLaunchKernelGGL(K_units, dim3(nblk(p->n_bc, 4)), dim3(256), 0, st, unit_args(p, d));
+  hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(256), 0, st, left_args(p, d));
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -1593,7 +1735,7 @@ int mpc_rows(mpc_plan* p, void* stream) {
   size_t tb = p->cub_tmp;
   HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, d.diff, d.depth, (int)p->G, st));
   hipLaunchKernelGGL(K_assemble, dim3(nblk(p->G, 4)), dim3(256), 0, st, d);
-  hipLaunchKernelGGL(K_strings, dim3(strings_grid(p->N)), dim3(256), 0, st, str_args(d));
+  hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(256), 0, st, flank_args(p, d));
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -1626,10 +1768,10 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
       launch_parse(p, d, st);
       break;
     case MPC_K_LEFT:
-      hipLaunchKernelGGL(K_left, dim3(p->n_left_wg), dim3(256), 0, st, left_args(p, d));
+      hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(256), 0, st, left_args(p, d));
       break;
-    case MPC_K_STRINGS:
-      hipLaunchKernelGGL(K_strings, dim3(strings_grid(p->N)), dim3(256), 0, st, str_args(d));
+    case MPC_K_FLANK:
+      hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(256), 0, st, flank_args(p, d));
       break;
     default:
       return fail(MPC_E_ARG, "unknown kernel");

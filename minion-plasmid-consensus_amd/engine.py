@@ -21,7 +21,7 @@ DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL = 1, 2, 4, 8, 16, 32
 
 DE_NAMES = {DE_OP: "Unknown operator", DE_VALUE: "ValueError", DE_INDEX: "IndexError", DE_KEY: "KeyError",
             DE_CAPACITY: "row capacity", DE_INTERNAL: "internal invariant"}
-K_PARSE, K_ODD, K_LEFT, K_STRINGS = 0, 1, 2, 3
+K_PARSE, K_ODD, K_LEFT, K_FLANK = 0, 1, 2, 3
 CS_PAD = 2048  # readable bytes required past the end of the cs buffer (mpc.h)
 FLANK_PAD = 16  # readable bytes required past the end of the up/down buffers (mpc.h)
 

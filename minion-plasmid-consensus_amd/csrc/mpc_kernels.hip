@@ -1451,6 +1451,22 @@ static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
   return a;
 }
 
+// One launch clears every accumulator of a run (status, bitmaps, tallies).
+struct ClearArgs {
+  uint32_t* ptr[12];
+  int64_t words[12];
+  uint32_t value[12];
+  int32_t n;
+};
+__global__ __launch_bounds__(256) void K_clear(ClearArgs c) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int k = 0; k < c.n; ++k) {
+    uint32_t* p = c.ptr[k];
+    const uint32_t v = c.value[k];
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < c.words[k]; i += stride) p[i] = v;
+  }
+}
+
 static inline unsigned nblk(int64_t n, int b = 256) {
   int64_t g = (n + b - 1) / b;
   if (g < 1) g = 1;
@@ -1668,12 +1684,22 @@ int mpc_parse(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  HIPCHK(hipMemsetAsync(d.status, 0, 4 * MPC_ST_WORDS, st));
-  HIPCHK(hipMemsetAsync(d.status + MPC_ST_FIRST_READ, 0xff, 4, st));
-  HIPCHK(hipMemsetAsync(d.hasleft, 0, p->sz[mpc_plan::B_HASLEFT], st));
-  HIPCHK(hipMemsetAsync(d.ovf_cnt, 0, 4, st));
-  HIPCHK(hipMemsetAsync(d.diff, 0, 4 * p->G, st));
-  HIPCHK(hipMemsetAsync(d.sub, 0, 16 * p->G, st));
+  {
+    ClearArgs c{};
+    auto add = [&](void* ptr, int64_t words, uint32_t v) {
+      c.ptr[c.n] = reinterpret_cast<uint32_t*>(ptr); c.words[c.n] = words; c.value[c.n] = v; ++c.n;
+    };
+    add(d.status, MPC_ST_FIRST_READ, 0u);                // (disjoint ranges: no ordering between threads)
+    add(d.status + MPC_ST_FIRST_READ, 1, 0xffffffffu);
+    add(d.status + MPC_ST_FIRST_READ + 1, MPC_ST_WORDS - MPC_ST_FIRST_READ - 1, 0u);
+    add(d.hasleft, (int64_t)(p->sz[mpc_plan::B_HASLEFT] / 4), 0u);
+    add(d.ovf_cnt, 1, 0u);
+    add(d.diff, p->G, 0u);
+    add(d.sub, 4 * p->G, 0u);
+    add(d.maxR, p->G, 0u);
+    add(d.maxdepth, p->S, 0u);
+    hipLaunchKernelGGL(K_clear, dim3(nblk(4 * p->G, 256) < 512 ? nblk(4 * p->G, 256) : 512), dim3(256), 0, st, c);
+  }
   if (p->n_parse_wg > 0)
     launch_parse(p, d, st);
   HIPCHK(hipGetLastError());
@@ -1684,7 +1710,6 @@ int mpc_index(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  HIPCHK(hipMemsetAsync(d.maxR, 0, 4 * p->G, st));
   if (p->N > 0) hipLaunchKernelGGL(K_rsplit, dim3(nblk(p->N)), dim3(256), 0, st, d, p->sentinel);
   if (p->Ng > 0) {
     size_t tb = p->cub_tmp;
@@ -1747,7 +1772,6 @@ int mpc_consensus(mpc_plan* p, double mdf, double gtf, void* stream) {
   d.mdf = mdf;
   d.gtf = gtf;
   const int64_t R = p->row_cap;
-  HIPCHK(hipMemsetAsync(d.maxdepth, 0, 4 * p->S, st));
   hipLaunchKernelGGL(K_call, dim3(nblk(R)), dim3(256), 0, st, d, R);
   hipLaunchKernelGGL(K_keep, dim3(nblk(R)), dim3(256), 0, st, d, R);
   uint8_t* tmp = at<uint8_t>(p, mpc_plan::B_CUB);

@@ -42,7 +42,6 @@ constexpr uint32_t DE_OP = MPC_DE_OP, DE_VALUE = MPC_DE_VALUE, DE_INDEX = MPC_DE
 
 constexpr int kBlk = 1024;          // cs bytes staged per wave iteration (64 lanes x 16 B)
 constexpr int kInsInline = 4;       // insertions up to this length travel as one event word
-constexpr int kFSlots = 4;          // right-justified insertion slots tallied per run (== kInsInline)
 constexpr int kMaxRefLen = (1 << 22) - 1;
 constexpr int kAdvCap = 1 << 22;    // > any reference length: a clamped advance keeps i past the end
 constexpr int kLaneCap = 1 << 24;   // saturation of one lane's advance sum (64 lanes stay < 2^31)
@@ -95,7 +94,6 @@ struct Dev {  // device-side views of the plan for the small kernels (passed by 
   int32_t* diff;                     // [G]
   uint32_t* sub;                     // [G][4]
   int32_t* M;                        // [Ng+G] per run
-  uint32_t* F;                       // [Ng+G][16]
   int32_t* hflag; int32_t* hscan; int32_t* segR; int32_t* seg_lo; int32_t* seg_hi; int32_t* seg_run;
   int32_t* lo_f; int32_t* rowcnt; int32_t* row_base;
   int32_t* depth;
@@ -709,9 +707,6 @@ __global__ __launch_bounds__(256) void K_zero_runs(Dev d) {
   const int64_t nruns = (int64_t)d.right_start[d.G] + d.G;
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nruns; t += (int64_t)gridDim.x * blockDim.x) {
     d.M[t] = 0;
-    const uint4 z = make_uint4(0, 0, 0, 0);
-    uint4* f = reinterpret_cast<uint4*>(d.F + t * 16);
-    f[0] = z; f[1] = z; f[2] = z; f[3] = z;
   }
 }
 
@@ -805,12 +800,13 @@ __device__ __forceinline__ int64_t unit_event_src(const int32_t* s_pre, const in
 }
 
 // ---------------------------------------------------------------------------
-// K_left: LEFT events -> per-run max length M and right-justified insertion
-// tallies F.  Persistent workgroups over the work units: a unit's events all
-// lie in one 16-gap bucket, so its (gap, run) counters live in LDS (runs
-// k < kKMax; rarer runs go to HBM) and are flushed with atomics (several units
-// may share a bucket).  Upstream flanks are LEFT events too: their length
-// feeds M.  Long insertions (grid-stride tail) only update M.
+// K_left: LEFT events -> per-run max length M (the slot layout's input; the
+// bases themselves are tallied on rows by K_flank once the layout is known).
+// Persistent workgroups over the work units: a unit's events all lie in one
+// 16-gap bucket, so its (gap, run) maxima live in LDS (runs k < kKMax; rarer
+// runs go to HBM) and are flushed with atomics (several units may share a
+// bucket).  Insertions and upstream flanks are LEFT events; long insertions
+// (grid-stride tail) too.
 // ---------------------------------------------------------------------------
 struct LeftArgs {
   const int64_t* up_off; const int32_t* sample;
@@ -820,12 +816,11 @@ struct LeftArgs {
   int64_t N, read_offset, ovf_cap;
   int32_t nbs;
   const int32_t* right_start; const int32_t* vals_out;
-  int32_t* M; uint32_t* F;
+  int32_t* M;
   const Ovf* ovf; const uint32_t* ovf_cnt;
 };
 
 __global__ __launch_bounds__(256) void K_left(LeftArgs a) {
-  __shared__ uint32_t Fl[kBW][kKMax][16];
   __shared__ uint32_t Ml[kBW][kKMax];
   __shared__ int32_t s_pre[256];
   __shared__ int64_t s_src[256];
@@ -834,7 +829,6 @@ __global__ __launch_bounds__(256) void K_left(LeftArgs a) {
   // (K_units raises DE_INTERNAL instead of overrunning the unit list)
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
-    for (int k = threadIdx.x; k < kBW * kKMax * 16; k += blockDim.x) (&Fl[0][0][0])[k] = 0;
     for (int k = threadIdx.x; k < kBW * kKMax; k += blockDim.x) (&Ml[0][0])[k] = 0;
     {
       const int4 bc = a.bc[a.units[u].x];
@@ -866,35 +860,14 @@ __global__ __launch_bounds__(256) void K_left(LeftArgs a) {
       }
       const int32_t ra = s_rs[gap - g0], rb = s_rs[gap - g0 + 1];
       const int64_t k = rb > ra ? lower_bound_i32(a.vals_out, ra, rb, (int32_t)rg) - ra : 0;
-      const int64_t run = ra + g + k;
-      const bool ins = !(ev & kFlankBit);
-      if (k < kKMax) {
-        atomicMax(&Ml[gap - g0][k], (uint32_t)L);
-        if (ins)
-          for (int bi = 0; bi < L; ++bi) {  // bi counts from the 3' end (:55-61)
-            const int code = (int)((ev >> (2 * (L - 1 - bi))) & 3u);
-            atomicAdd(&Fl[gap - g0][k][bi * 4 + code], 1u);
-          }
-      } else {
-        atomicMax(a.M + run, L);
-        if (ins)
-          for (int bi = 0; bi < L; ++bi) {
-            const int code = (int)((ev >> (2 * (L - 1 - bi))) & 3u);
-            atomicAdd(a.F + run * 16 + bi * 4 + code, 1u);
-          }
-      }
+      if (k < kKMax) atomicMax(&Ml[gap - g0][k], (uint32_t)L);
+      else atomicMax(a.M + ra + g + k, L);
     }
     __syncthreads();
-    // flush: lanes sweep (gap, run, field) so each 16-field row is contiguous
-    for (int q = threadIdx.x; q < kBW * kKMax * 16; q += blockDim.x) {
-      const int f = q & 15, k = (q >> 4) % kKMax, p = q / (16 * kKMax);
+    for (int q = threadIdx.x; q < kBW * kKMax; q += blockDim.x) {
+      const int k = q % kKMax, p = q / kKMax;
       const uint32_t m = Ml[p][k];
-      if (!m) continue;
-      const int64_t g = (int64_t)gb + g0 + p;
-      const int64_t run = s_rs[p] + g + k;
-      if (f == 0) atomicMax(a.M + run, (int32_t)m);
-      const uint32_t v = Fl[p][k][f];
-      if (v) atomicAdd(a.F + run * 16 + f, v);
+      if (m) atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + k, (int32_t)m);
     }
     __syncthreads();
   }
@@ -976,15 +949,11 @@ __global__ void K_rows_total(Dev d) {
 }
 
 // ---------------------------------------------------------------------------
-// Rows: one wave per gap writes the gap's slot rows (F contributions summed in
-// LDS, plain stores) and the odd-position row that follows it.
+// Rows: one wave per gap zeroes the gap's slot rows (K_flank adds the
+// insertion and flank bases) and writes the odd-position row that follows it.
 // ---------------------------------------------------------------------------
-constexpr int kAsmChunk = 128;  // rows per LDS chunk per wave
-
 __global__ __launch_bounds__(256) void K_assemble(Dev d) {
-  __shared__ uint32_t s_rows[4][kAsmChunk * 4];
   const int l = lane(), w = threadIdx.x >> 6;
-  uint32_t* acc = s_rows[w];
   if (d.status[MPC_ST_FLAGS] & DE_CAP) return;
   const int64_t stride = (int64_t)gridDim.x * 4;
   for (int64_t g = (int64_t)blockIdx.x * 4 + w; g < d.G; g += stride) {
@@ -993,41 +962,10 @@ __global__ __launch_bounds__(256) void K_assemble(Dev d) {
     const int64_t p = g - d.gbase[s];
     const int64_t n = d.n_of[s];
     const int64_t rb = d.row_base[g];
-    const int32_t lo = d.lo_f[g];
     const int64_t nslots = (int64_t)d.rowcnt[g] - (p < n ? 1 : 0);
-    const int64_t r0 = d.right_start[g] + g, r1 = d.right_start[g + 1] + g + 1;
-    for (int64_t c0 = 0; c0 < nslots; c0 += kAsmChunk) {
-      const int64_t cn = nslots - c0 < kAsmChunk ? nslots - c0 : kAsmChunk;
-      for (int k = l; k < kAsmChunk * 4; k += 64) acc[k] = 0;
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      // F contributions: LEFT run with hi at its segment
-      for (int64_t run = r0 + l; run < r1; run += 64) {
-        const int32_t m = d.M[run];
-        if (m <= 0) continue;
-        const int32_t hi = d.seg_hi[d.hscan[run] - 1];
-        const int bmax = m < kFSlots ? m : kFSlots;
-        for (int bi = 0; bi < bmax; ++bi) {
-          const int64_t slot = (int64_t)lo + hi - 1 - bi - c0;
-          if (slot < 0 || slot >= cn) continue;
-          for (int c = 0; c < 4; ++c) {
-            const uint32_t v = d.F[run * 16 + bi * 4 + c];
-            if (v) atomicAdd(acc + slot * 4 + c, v);
-          }
-        }
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      for (int64_t k = l; k < cn; k += 64) {
-        const uint4 v = make_uint4(acc[k * 4], acc[k * 4 + 1], acc[k * 4 + 2], acc[k * 4 + 3]);
-        reinterpret_cast<uint4*>(d.rows)[rb + c0 + k] = v;
-        d.meta[rb + c0 + k] = (c0 + k == 0) ? 2 : 0;
-      }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    for (int64_t k = l; k < nslots; k += 64) {
+      reinterpret_cast<uint4*>(d.rows)[rb + k] = make_uint4(0, 0, 0, 0);
+      d.meta[rb + k] = (k == 0) ? 2 : 0;
     }
     if (p < n && l == 0) {
       // odd position p: depth = reads covering p with a match or substitution
@@ -1051,12 +989,12 @@ __global__ __launch_bounds__(256) void K_assemble(Dev d) {
 }
 
 // ---------------------------------------------------------------------------
-// Flank tallies (:37-72 applied to the flank strings).  Every flank base lands
-// in the slot block of its anchor gap, so a workgroup owns one 16-gap bucket
-// (and a chunk of the parse workgroups whose bucketed flank events it reads):
-// it tallies the bucket's row range in a dense LDS histogram, bytes processed
-// flat across events, then flushes with global atomics (hot buckets are split
-// over several workgroups).  A grid-stride tail adds the long insertions.
+// Slot tallies of the even positions (:37-72 applied to insertions and flank
+// strings).  Every inserted / flank base lands in the slot block of its anchor
+// gap, so a work unit (events of one 16-gap bucket) tallies the bucket's row
+// range in a dense LDS histogram -- bases processed flat across events, 4 per
+// lane -- then flushes with global atomics (hot buckets are split over several
+// units).  A grid-stride tail adds the long insertions.
 // ---------------------------------------------------------------------------
 constexpr int kFlankRows = 2048;  // dense LDS rows per unit (else HBM atomics)
 
@@ -1092,12 +1030,11 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
   // (K_units raises DE_INTERNAL instead of overrunning the unit list)
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
-    {  // flank units only
+    {
       const int4 bc = a.bc[a.units[u].x];
       const int nn = a.n_of[bc.x];
       const int nbk0 = (nn + 1 + kBW - 1) / kBW;
-      if (bc.y < nbk0) continue;
-      const int gg0 = (bc.y - nbk0) * kBW;
+      const int gg0 = (bc.y >= nbk0 ? bc.y - nbk0 : bc.y) * kBW;
       const int gl = gg0 + kBW - 1 < nn ? gg0 + kBW - 1 : nn;
       const int64_t gbb = a.gbase[bc.x];
       if (tid <= gl + 1 - gg0) s_rs[tid] = a.right_start[gbb + gg0 + tid];
@@ -1112,13 +1049,14 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
     const int n = a.n_of[uv.smp];
     const int64_t gb = a.gbase[uv.smp];
     const int nbk = (n + 1 + kBW - 1) / kBW;
-    const int g0 = (uv.bucket - nbk) * kBW;
+    const int g0 = (uv.bucket >= nbk ? uv.bucket - nbk : uv.bucket) * kBW;
     const int gl = (g0 + kBW - 1 < n ? g0 + kBW - 1 : n);  // last gap of the bucket
     const int64_t R0 = s_rowb[0];
     const int64_t R1 = (int64_t)s_rowb[gl - g0] + a.rowcnt[gb + gl];
     const bool dense = R1 - R0 <= kFlankRows;
     if (dense)
       for (int k = tid; k < (int)(R1 - R0) * 4; k += blockDim.x) cnt[k] = 0;
+    __syncthreads();
     for (int e0 = uv.e0; e0 < uv.e0 + uv.cnt; e0 += 256) {
       // one event per thread: anchor row and flank byte range
       const int e = e0 + tid;
@@ -1126,12 +1064,14 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
       int64_t off = 0, anc = 0;
       bool down = false;
       int64_t r = 0;
+      bool ins = false;
       if (e < uv.e0 + uv.cnt) {
         const uint64_t ev = a.ins_sorted[unit_event_src(s_pre, s_src, e)];
         const int gap = (int)((ev >> 10) & kNullGap);
         const int p = gap - g0;
         const int64_t rg = event_read(ev);
         r = rg - a.read_offset;
+        ins = !(ev & kFlankBit);
         down = (ev & kDownBit) != 0;
         const int64_t g = gb + gap;
         const int32_t ra = s_rs[p], rb = s_rs[p + 1];
@@ -1143,8 +1083,19 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
             hi = a.seg_hi[a.hscan[ra + g + k] - 1];
           }
           anc = (int64_t)s_rowb[p] + s_lof[p] + hi - 1;
-          off = a.up_off[r];
-          L = a.up_off[r + 1] - off;
+          if (ins) {  // inline insertion: 2-bit codes in the event word, string order; tallied here
+            const int Li = (int)((ev >> 8) & 3u) + 1;
+            for (int k = 0; k < Li; ++k) {
+              const int code = (int)((ev >> (2 * k)) & 3u);
+              const int64_t row = anc - (Li - 1 - k);
+              if (dense && row >= R0 && row < R1) atomicAdd(cnt + (row - R0) * 4 + code, 1u);
+              else atomicAdd(a.rows + row * 4 + code, 1u);
+            }
+            L = 0;
+          } else {
+            off = a.up_off[r];
+            L = a.up_off[r + 1] - off;
+          }
         } else {      // RIGHT at gap i_end: base bi -> row lo - lo_at + bi
           int64_t lo_at = 0;
           bool ok = true;
@@ -1186,8 +1137,8 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
         const int b0 = 4 * (x - e_pre[lo]);
         const int L = e_len[lo];
         const bool dn = e_down[lo] != 0;
-        const uint8_t* src8 = (dn ? a.down : a.up) + e_off[lo];
         uint32_t c4[4];
+        const uint8_t* src8 = (dn ? a.down : a.up) + e_off[lo];
 #pragma unroll
         for (int k = 0; k < 4; ++k) c4[k] = b0 + k < L ? src8[b0 + k] : 0u;
         const int64_t anc = e_anc[lo];
@@ -1351,7 +1302,7 @@ struct mpc_plan {
   bool fused = false;
   enum {
     B_STATUS, B_NOF, B_GBASE, B_IEND, B_INSRAW, B_INSSORT, B_BKCNT, B_BKOFF, B_RBASE, B_OVF, B_OVFCNT,
-    B_HASLEFT, B_MAXR, B_KIN, B_VIN, B_KOUT, B_VOUT, B_RLEN, B_RPOS, B_RSTART, B_DIFF, B_SUB, B_M, B_F,
+    B_HASLEFT, B_MAXR, B_KIN, B_VIN, B_KOUT, B_VOUT, B_RLEN, B_RPOS, B_RSTART, B_DIFF, B_SUB, B_M,
     B_HFLAG, B_HSCAN, B_SEGR, B_SEGLO, B_SEGHI, B_SEGRUN, B_LOF, B_ROWCNT, B_ROWBASE, B_DEPTH, B_ROWS,
     B_META, B_RES, B_KEEP, B_KEEPSCAN, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_CUB, B_COUNT
   };
@@ -1378,7 +1329,7 @@ Dev mpc_plan::dev() const {
   d.keys_out = at<uint32_t>(this, B_KOUT); d.vals_out = at<int32_t>(this, B_VOUT);
   d.rlen = at<int32_t>(this, B_RLEN); d.rpos = at<int32_t>(this, B_RPOS); d.right_start = at<int32_t>(this, B_RSTART);
   d.diff = at<int32_t>(this, B_DIFF); d.sub = at<uint32_t>(this, B_SUB);
-  d.M = at<int32_t>(this, B_M); d.F = at<uint32_t>(this, B_F);
+  d.M = at<int32_t>(this, B_M);
   d.hflag = at<int32_t>(this, B_HFLAG); d.hscan = at<int32_t>(this, B_HSCAN);
   d.segR = at<int32_t>(this, B_SEGR); d.seg_lo = at<int32_t>(this, B_SEGLO); d.seg_hi = at<int32_t>(this, B_SEGHI);
   d.seg_run = at<int32_t>(this, B_SEGRUN);
@@ -1421,7 +1372,7 @@ static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
   a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
   a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = 2 * p->nbmax;
-  a.right_start = d.right_start; a.vals_out = d.vals_out; a.M = d.M; a.F = d.F;
+  a.right_start = d.right_start; a.vals_out = d.vals_out; a.M = d.M;
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt;
   return a;
 }
@@ -1588,7 +1539,6 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_DIFF, G, 4);
   set(mpc_plan::B_SUB, G * 4, 4);
   set(mpc_plan::B_M, RU, 4);
-  set(mpc_plan::B_F, RU * 16, 4);
   set(mpc_plan::B_HFLAG, RU, 4);
   set(mpc_plan::B_HSCAN, RU, 4);
   set(mpc_plan::B_SEGR, RU, 4);

@@ -78,7 +78,7 @@ def main():
     samples = [syn.sample(s) for s in range(2 if antisense else 1)]
     if world > 1:
         dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
-        runner = dmod.ShardedPileup(samples, rank=rank, world=world, device=local)
+        runner = dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange())
     else:
         runner = eng.Runner(samples, device=local)
     batch = runner.batch

@@ -39,7 +39,7 @@
 extern "C" {
 #endif
 
-#define MPC_ABI_VERSION 1
+#define MPC_ABI_VERSION 2
 
 /* return codes */
 #define MPC_OK 0
@@ -89,9 +89,13 @@ typedef struct {
   int64_t n_reads;             /* local reads */
   int64_t cs_bytes;            /* cs_off[n_reads] - cs_off[0] */
   int64_t cs_base;             /* cs_off[0] */
-  /* multi-GPU read sharding (single GPU: 0, n_reads) */
+  /* multi-GPU read sharding (single GPU: 0, n_reads, 0, 1).  Shards own
+   * CONTIGUOUS global read ranges in shard order (the slot layout at gaps with
+   * both LEFT and RIGHT events depends on read order). */
   int64_t read_offset;         /* global index of local read 0 */
   int64_t n_reads_global;
+  int32_t shard;               /* this shard's index */
+  int32_t n_shards;            /* number of shards (0 is taken as 1) */
 } mpc_input;
 
 typedef struct mpc_plan mpc_plan;
@@ -104,11 +108,14 @@ enum {
   MPC_BUF_MAXDEPTH,     /* uint32[n_samples] */
   MPC_BUF_ROWS,         /* uint32[rows][4]: per-slot A,T,C,G tallies in output order */
   MPC_BUF_ROWMETA,      /* uint8[rows] bit0 odd position, bit1 first slot of its position */
-  MPC_BUF_RIGHT_KEY,    /* uint32[n_reads_global] mixed downstream keys (multi-GPU exchange) */
-  MPC_BUF_RIGHT_READ,   /* int32[n_reads_global] */
-  MPC_BUF_HASLEFT,      /* uint32[(gaps+31)/32 + 1] bitmap: gap holds a LEFT event */
-  MPC_BUF_MAXR,         /* int32[gaps] */
-  MPC_BUF_RUN_M,        /* int32[n_reads_global + gaps] */
+  MPC_BUF_RIGHT_CNT,    /* int32[gaps] this shard's mixed RIGHT events per gap     (exchange: all-gather) */
+  MPC_BUF_RIGHT_CNT_ALL,/* int32[n_shards][gaps] all shards' MPC_BUF_RIGHT_CNT   (exchange: target)     */
+  MPC_BUF_HASLEFT,      /* uint32[(gaps+31)/32 + 1] bitmap: gap holds a LEFT event (exchange: OR)         */
+  MPC_BUF_MAXR,         /* int32[gaps] longest RIGHT event at RIGHT-only gaps       (exchange: MAX)        */
+  MPC_BUF_RUN_M,        /* int32[n_reads_global + gaps] longest LEFT event per run  (exchange: MAX)        */
+  MPC_BUF_SEG_R,        /* int32[n_reads_global + gaps] longest RIGHT event per segment (exchange: MAX)    */
+  MPC_BUF_DIFF,         /* int32[gaps] read-span/deletion difference array          (exchange: SUM)        */
+  MPC_BUF_SUB,          /* uint32[gaps][4] substitution tallies                     (exchange: SUM)        */
   MPC_BUF_COUNT
 };
 
@@ -127,13 +134,23 @@ int mpc_plan_buffer(const mpc_plan* plan, int which, size_t* byte_offset, int64_
 /* update the per-read device pointers (same shape) without re-planning */
 int mpc_plan_set_input(mpc_plan* plan, const mpc_input* in);
 
-/* Phases (single GPU: mpc_run() = all of them).  Between phases a multi-GPU
- * host inserts the collectives described in DESIGN.md §Multi-GPU. */
-int mpc_parse(mpc_plan* plan, void* stream);        /* cs -> events, i_end, LEFT marks        */
-int mpc_index(mpc_plan* plan, void* stream);        /* downstream keys, stable sort, runs      */
-int mpc_tally(mpc_plan* plan, void* stream);        /* odd tallies, insertion tallies, run M   */
-int mpc_layout(mpc_plan* plan, void* stream);       /* even-slot replay, row offsets           */
-int mpc_rows(mpc_plan* plan, void* stream);         /* depth, row assembly, flank tallies      */
+/* Phases (single GPU: mpc_run() = all of them, in this order).  With
+ * n_shards > 1 the host inserts these collectives (Multi-GPU):
+ *   mpc_parse    ; OR  HASLEFT, SUM DIFF/SUB (may be deferred to before rows)
+ *   mpc_index    ; ALL-GATHER RIGHT_CNT -> RIGHT_CNT_ALL, MAX MAXR
+ *   mpc_runs     (global run index space)
+ *   mpc_tally    ; MAX RUN_M
+ *   mpc_segments ; MAX SEG_R
+ *   mpc_layout   (identical on every shard)
+ *   mpc_rows     ; SUM ROWS  (odd rows come from shard 0, others add flank / insertion bases)
+ *   mpc_consensus (identical on every shard) */
+int mpc_parse(mpc_plan* plan, void* stream);        /* cs -> events, i_end, LEFT marks, tallies  */
+int mpc_index(mpc_plan* plan, void* stream);        /* mixed downstream keys, stable sort        */
+int mpc_runs(mpc_plan* plan, void* stream);         /* global run index space, clear run maxima  */
+int mpc_tally(mpc_plan* plan, void* stream);        /* work units, run M                         */
+int mpc_segments(mpc_plan* plan, void* stream);     /* segments, RIGHT maxima per segment        */
+int mpc_layout(mpc_plan* plan, void* stream);       /* even-slot replay, row offsets             */
+int mpc_rows(mpc_plan* plan, void* stream);         /* depth, odd rows, slot (flank/ins) tallies */
 int mpc_consensus(mpc_plan* plan, double min_depth_factor, double global_threshold_factor,
                   void* stream);                    /* max depth, calls, compaction            */
 int mpc_run(mpc_plan* plan, double min_depth_factor, double global_threshold_factor, void* stream);

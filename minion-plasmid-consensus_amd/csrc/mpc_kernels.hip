@@ -90,7 +90,12 @@ struct Dev {  // device-side views of the plan for the small kernels (passed by 
   uint32_t* keys_in; int32_t* vals_in; uint32_t* keys_out; int32_t* vals_out;
   int32_t* rlen;                     // [Ng] downstream length by global read
   int32_t* rpos;                     // [N] local read -> position of its mixed RIGHT event in the sorted list
-  int32_t* right_start;              // [G+1]
+  int32_t* right_start;              // [G+1] mixed RIGHT events (all shards) with gap < g
+  int32_t* rsl;                      // [G+1] the same over this shard's sorted list (== right_start on 1 GPU)
+  int32_t* roff;                     // [G+1] mixed RIGHT events at gap g on lower shards
+  int32_t* rcnt;                     // [G] this shard's mixed RIGHT events per gap (exchange)
+  const int32_t* rcnt_all;           // [n_shards][G] all shards' counts (exchange)
+  int32_t shard, n_shards;
   int32_t* diff;                     // [G]
   uint32_t* sub;                     // [G][4]
   int32_t* M;                        // [Ng+G] per run
@@ -691,13 +696,19 @@ __global__ __launch_bounds__(256) void K_rsplit(Dev d, uint32_t sentinel) {
   peel_atomic_max(d.maxR, g < 0 ? 0 : g, len, in && g >= 0 && !mixed);
 }
 
-// right_start[g] = #mixed RIGHT events with gap < g; rpos[local read] = its
-// position in the sorted list (so consumers need no search)
+// rsl[g] = #mixed RIGHT events of this shard with gap < g; rpos[local read] =
+// its position in the shard's sorted list (so consumers need no search).  One
+// shard: right_start = rsl, roff = 0.  Several: per-gap counts for the exchange.
 __global__ __launch_bounds__(256) void K_rstart(Dev d) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (t <= d.G) d.right_start[t] = (int32_t)lower_bound_u32(d.keys_out, 0, d.Ng, (uint32_t)t);
-  if (t == 0) d.status[MPC_ST_MIXED] = (uint32_t)lower_bound_u32(d.keys_out, 0, d.Ng, (uint32_t)d.G);
-  if (t < d.Ng && d.keys_out[t] < (uint32_t)d.G) {
+  if (t <= d.G) {
+    const int32_t v = (int32_t)lower_bound_u32(d.keys_out, 0, d.N, (uint32_t)t);
+    d.rsl[t] = v;
+    if (d.n_shards == 1) { d.right_start[t] = v; d.roff[t] = 0; }
+    if (t < d.G) d.rcnt[t] = (int32_t)lower_bound_u32(d.keys_out, 0, d.N, (uint32_t)t + 1) - v;
+  }
+  if (t == 0) d.status[MPC_ST_MIXED] = (uint32_t)lower_bound_u32(d.keys_out, 0, d.N, (uint32_t)d.G);
+  if (t < d.N && d.keys_out[t] < (uint32_t)d.G) {
     const int64_t lr = (int64_t)d.vals_out[t] - d.read_offset;
     if (lr >= 0 && lr < d.N) d.rpos[lr] = (int32_t)t;
   }
@@ -710,15 +721,45 @@ __global__ __launch_bounds__(256) void K_zero_runs(Dev d) {
   }
 }
 
-// run index of a LEFT event of global read rg at global gap g: runs of gap g
-// are [right_start[g] + g, right_start[g+1] + g + 1); run k follows the k-th
-// mixed RIGHT event (the RIGHT event of read r comes after r's own LEFT events,
-// :303-323).
-__device__ __forceinline__ int64_t run_of2(const int32_t* right_start, const int32_t* vals_out, int64_t g, int64_t rg) {
-  const int64_t lo = right_start[g], hi = right_start[g + 1];
-  int64_t k = 0;
-  if (hi > lo) k = lower_bound_i32(vals_out, lo, hi, (int32_t)rg) - lo;
-  return lo + g + k;
+// Several shards: global right_start and roff from all shards' per-gap counts
+// (one workgroup, block scan over the gaps).
+__global__ __launch_bounds__(1024) void K_runs(Dev d) {
+  __shared__ int32_t s_w[16];
+  __shared__ int32_t s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  const int l = lane(), w = threadIdx.x >> 6;
+  for (int64_t c0 = 0; c0 <= d.G; c0 += blockDim.x) {
+    const int64_t g = c0 + threadIdx.x;
+    int32_t tot = 0, below = 0;
+    if (g < d.G)
+      for (int k = 0; k < d.n_shards; ++k) {
+        const int32_t c = d.rcnt_all[(int64_t)k * d.G + g];
+        tot += c;
+        if (k < d.shard) below += c;
+      }
+    const int inc = wave_scan_i32(tot);
+    if (l == 63) s_w[w] = inc;
+    __syncthreads();
+    int pre = s_carry;
+    for (int k = 0; k < w; ++k) pre += s_w[k];
+    if (g <= d.G) { d.right_start[g] = pre + inc - tot; d.roff[g] = below; }
+    __syncthreads();
+    if (threadIdx.x == blockDim.x - 1) s_carry = pre + inc;
+    __syncthreads();
+  }
+}
+
+// Global run index of a LEFT event of (this shard's) global read rg at global
+// gap g: runs of gap g are [right_start[g] + g, right_start[g+1] + g + 1); run
+// k follows the k-th mixed RIGHT event of the gap, k = RIGHT events of lower
+// shards + this shard's RIGHT events of earlier reads.
+__device__ __forceinline__ int64_t run_left(const int32_t* rs, const int32_t* rsl, const int32_t* roff,
+                                            const int32_t* vals_out, int64_t g, int64_t rg) {
+  const int64_t a = rsl[g], b = rsl[g + 1];
+  int64_t k = roff[g];
+  if (b > a) k += lower_bound_i32(vals_out, a, b, (int32_t)rg) - a;
+  return rs[g] + g + k;
 }
 
 // ---------------------------------------------------------------------------
@@ -815,7 +856,7 @@ struct LeftArgs {
   const uint64_t* ins_sorted; const int32_t* bk_cnt; const int32_t* bk_off; const int64_t* rbase;
   int64_t N, read_offset, ovf_cap;
   int32_t nbs;
-  const int32_t* right_start; const int32_t* vals_out;
+  const int32_t* right_start; const int32_t* rsl; const int32_t* roff; const int32_t* vals_out;
   int32_t* M;
   const Ovf* ovf; const uint32_t* ovf_cnt;
 };
@@ -825,7 +866,7 @@ __global__ __launch_bounds__(256) void K_left(LeftArgs a) {
   __shared__ int32_t s_pre[256];
   __shared__ int64_t s_src[256];
   __shared__ int32_t s_wsum[4];
-  __shared__ int32_t s_rs[kBW + 1];  // right_start of the bucket's gaps
+  __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1];  // per gap of the bucket
   // (K_units raises DE_INTERNAL instead of overrunning the unit list)
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
@@ -836,7 +877,12 @@ __global__ __launch_bounds__(256) void K_left(LeftArgs a) {
       const int nbk0 = (nn + 1 + kBW - 1) / kBW;
       const int gg0 = (bc.y >= nbk0 ? bc.y - nbk0 : bc.y) * kBW;
       const int gl = gg0 + kBW - 1 < nn ? gg0 + kBW - 1 : nn;
-      if ((int)threadIdx.x <= gl + 1 - gg0) s_rs[threadIdx.x] = a.right_start[a.gbase[bc.x] + gg0 + threadIdx.x];
+      if ((int)threadIdx.x <= gl + 1 - gg0) {
+        const int64_t g = a.gbase[bc.x] + gg0 + threadIdx.x;
+        s_rs[threadIdx.x] = a.right_start[g];
+        s_rsl[threadIdx.x] = a.rsl[g];
+        s_roff[threadIdx.x] = a.roff[g];
+      }
     }
     const UnitView uv = load_unit(a.bc, a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, s_pre, s_src, s_wsum);
     const int n = a.n_of[uv.smp];
@@ -858,10 +904,11 @@ __global__ __launch_bounds__(256) void K_left(LeftArgs a) {
       } else {
         L = (int)((ev >> 8) & 3u) + 1;
       }
-      const int32_t ra = s_rs[gap - g0], rb = s_rs[gap - g0 + 1];
-      const int64_t k = rb > ra ? lower_bound_i32(a.vals_out, ra, rb, (int32_t)rg) - ra : 0;
-      if (k < kKMax) atomicMax(&Ml[gap - g0][k], (uint32_t)L);
-      else atomicMax(a.M + ra + g + k, L);
+      const int p = gap - g0;
+      const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
+      const int64_t k = s_roff[p] + (lb > la ? lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la : 0);
+      if (k < kKMax) atomicMax(&Ml[p][k], (uint32_t)L);
+      else atomicMax(a.M + s_rs[p] + g + k, L);
     }
     __syncthreads();
     for (int q = threadIdx.x; q < kBW * kKMax; q += blockDim.x) {
@@ -877,7 +924,7 @@ __global__ __launch_bounds__(256) void K_left(LeftArgs a) {
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nov; t += nthreads) {
     const Ovf o = a.ovf[t];
     const int64_t g = (int64_t)a.gbase[a.sample[o.read]] + o.gap;
-    atomicMax(a.M + run_of2(a.right_start, a.vals_out, g, a.read_offset + o.read), o.len);
+    atomicMax(a.M + run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + o.read), o.len);
   }
 }
 
@@ -905,11 +952,12 @@ __global__ __launch_bounds__(256) void K_seg_heads(Dev d) {
 }
 
 __global__ __launch_bounds__(256) void K_seg_right(Dev d) {
-  const int64_t nm = d.right_start[d.G];
-  const int64_t nruns = nm + d.G;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nm; t += (int64_t)gridDim.x * blockDim.x) {
+  const int64_t nml = d.rsl[d.G];  // this shard's mixed RIGHT events
+  const int64_t nruns = (int64_t)d.right_start[d.G] + d.G;
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nml; t += (int64_t)gridDim.x * blockDim.x) {
     const int64_t g = d.keys_out[t];
-    const int64_t seg = d.hscan[t + g] - 1;  // segment of the run just before this RIGHT event
+    const int64_t tg = (int64_t)d.right_start[g] + d.roff[g] + (t - d.rsl[g]);  // position in the global list
+    const int64_t seg = d.hscan[tg + g] - 1;  // segment of the run just before this RIGHT event
     atomicMax(d.segR + seg, d.rlen[d.vals_out[t]]);
   }
   for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nruns; t += (int64_t)gridDim.x * blockDim.x)
@@ -967,7 +1015,10 @@ __global__ __launch_bounds__(256) void K_assemble(Dev d) {
       reinterpret_cast<uint4*>(d.rows)[rb + k] = make_uint4(0, 0, 0, 0);
       d.meta[rb + k] = (k == 0) ? 2 : 0;
     }
-    if (p < n && l == 0) {
+    if (p < n && l == 0 && d.shard != 0) {  // rows are summed over shards: odd rows come from shard 0
+      reinterpret_cast<uint4*>(d.rows)[rb + nslots] = make_uint4(0, 0, 0, 0);
+      d.meta[rb + nslots] = 3;
+    } else if (p < n && l == 0) {
       // odd position p: depth = reads covering p with a match or substitution
       const int64_t dep = d.depth[g];
       const uint32_t* sb = d.sub + g * 4;
@@ -1005,7 +1056,8 @@ struct FlankArgs {
   int64_t N, read_offset, ovf_cap;
   int32_t nbs;
   const int64_t* up_off; const uint8_t* up; const int64_t* down_off; const uint8_t* down;
-  const int32_t* right_start; const int32_t* vals_out; const int32_t* row_base; const int32_t* rowcnt;
+  const int32_t* right_start; const int32_t* rsl; const int32_t* roff; const int32_t* vals_out;
+  const int32_t* row_base; const int32_t* rowcnt;
   const int32_t* lo_f; const int32_t* seg_hi; const int32_t* seg_lo; const int32_t* hscan; const int32_t* rpos;
   uint32_t* rows; const Ovf* ovf; const uint32_t* ovf_cnt; const uint8_t* cs;
 };
@@ -1020,7 +1072,7 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
   __shared__ int32_t e_read[256];
   __shared__ uint8_t e_down[256];
   // per gap of the bucket: sorted-RIGHT range, row base, lo, hi of run 0
-  __shared__ int32_t s_rs[kBW + 1], s_rowb[kBW], s_lof[kBW], s_hi0[kBW];
+  __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1], s_rowb[kBW], s_lof[kBW], s_hi0[kBW];
   const int l = lane();
   const int w = uniform_i32((int)(threadIdx.x >> 6));
   const int tid = threadIdx.x;
@@ -1037,7 +1089,11 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
       const int gg0 = (bc.y >= nbk0 ? bc.y - nbk0 : bc.y) * kBW;
       const int gl = gg0 + kBW - 1 < nn ? gg0 + kBW - 1 : nn;
       const int64_t gbb = a.gbase[bc.x];
-      if (tid <= gl + 1 - gg0) s_rs[tid] = a.right_start[gbb + gg0 + tid];
+      if (tid <= gl + 1 - gg0) {
+        s_rs[tid] = a.right_start[gbb + gg0 + tid];
+        s_rsl[tid] = a.rsl[gbb + gg0 + tid];
+        s_roff[tid] = a.roff[gbb + gg0 + tid];
+      }
       if (tid <= gl - gg0) {
         const int64_t g = gbb + gg0 + tid;
         s_rowb[tid] = a.row_base[g];
@@ -1078,8 +1134,9 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
         int64_t L;
         if (!down) {  // LEFT at gap tstart: base bi (from the 3' end) -> row lo + hi_run - 1 - bi
           int32_t hi = s_hi0[p];
-          if (rb > ra) {  // mixed gap: run k = RIGHT events of earlier reads
-            const int64_t k = lower_bound_i32(a.vals_out, ra, rb, (int32_t)rg) - ra;
+          if (rb > ra) {  // mixed gap: run k = RIGHT events of earlier reads (all shards)
+            const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
+            const int64_t k = s_roff[p] + (lb > la ? lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la : 0);
             hi = a.seg_hi[a.hscan[ra + g + k] - 1];
           }
           anc = (int64_t)s_rowb[p] + s_lof[p] + hi - 1;
@@ -1099,10 +1156,11 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
         } else {      // RIGHT at gap i_end: base bi -> row lo - lo_at + bi
           int64_t lo_at = 0;
           bool ok = true;
-          if (rb > ra) {  // mixed gap: this read's RIGHT event in the sorted list
+          if (rb > ra) {  // mixed gap: this read's RIGHT event in the (global) sorted list
             const int64_t t = a.rpos[r];
-            ok = t >= ra && t < rb;
-            if (ok) lo_at = a.seg_lo[a.hscan[t + g] - 1];
+            const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
+            ok = t >= la && t < lb;
+            if (ok) lo_at = a.seg_lo[a.hscan[ra + s_roff[p] + (t - la) + g] - 1];
             else lerr |= DE_INTERNAL;
           }
           anc = (int64_t)s_rowb[p] + s_lof[p] - lo_at;
@@ -1167,7 +1225,7 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
   for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < nov; t += (int64_t)gridDim.x * 4) {
     const Ovf o = a.ovf[t];
     const int64_t g = a.gbase[a.sample[o.read]] + o.gap;
-    const int64_t run = run_of2(a.right_start, a.vals_out, g, a.read_offset + o.read);
+    const int64_t run = run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + o.read);
     const int64_t rb = (int64_t)a.row_base[g] + a.lo_f[g] + a.seg_hi[a.hscan[run] - 1] - 1;
     for (int64_t bi = l; bi < o.len; bi += 64) {
       const int c = code_upper(a.cs[o.off + o.len - 1 - bi]);
@@ -1299,10 +1357,11 @@ struct mpc_plan {
   std::vector<int32_t> work_parse, work_bc;  // int4 records
   int n_parse_wg = 0, parse_lds = 0, nbmax = 1;
   int64_t n_bc = 0, units_cap = 0;
+  int32_t shard = 0, n_shards = 1;
   bool fused = false;
   enum {
     B_STATUS, B_NOF, B_GBASE, B_IEND, B_INSRAW, B_INSSORT, B_BKCNT, B_BKOFF, B_RBASE, B_OVF, B_OVFCNT,
-    B_HASLEFT, B_MAXR, B_KIN, B_VIN, B_KOUT, B_VOUT, B_RLEN, B_RPOS, B_RSTART, B_DIFF, B_SUB, B_M,
+    B_HASLEFT, B_MAXR, B_KIN, B_VIN, B_KOUT, B_VOUT, B_RLEN, B_RPOS, B_RSTART, B_RSLOC, B_ROFF, B_RCNT, B_RCNTALL, B_DIFF, B_SUB, B_M,
     B_HFLAG, B_HSCAN, B_SEGR, B_SEGLO, B_SEGHI, B_SEGRUN, B_LOF, B_ROWCNT, B_ROWBASE, B_DEPTH, B_ROWS,
     B_META, B_RES, B_KEEP, B_KEEPSCAN, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_CUB, B_COUNT
   };
@@ -1328,6 +1387,8 @@ Dev mpc_plan::dev() const {
   d.keys_in = at<uint32_t>(this, B_KIN); d.vals_in = at<int32_t>(this, B_VIN);
   d.keys_out = at<uint32_t>(this, B_KOUT); d.vals_out = at<int32_t>(this, B_VOUT);
   d.rlen = at<int32_t>(this, B_RLEN); d.rpos = at<int32_t>(this, B_RPOS); d.right_start = at<int32_t>(this, B_RSTART);
+  d.rsl = at<int32_t>(this, B_RSLOC); d.roff = at<int32_t>(this, B_ROFF); d.rcnt = at<int32_t>(this, B_RCNT);
+  d.rcnt_all = at<int32_t>(this, B_RCNTALL); d.shard = shard; d.n_shards = n_shards;
   d.diff = at<int32_t>(this, B_DIFF); d.sub = at<uint32_t>(this, B_SUB);
   d.M = at<int32_t>(this, B_M);
   d.hflag = at<int32_t>(this, B_HFLAG); d.hscan = at<int32_t>(this, B_HSCAN);
@@ -1372,7 +1433,7 @@ static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
   a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
   a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = 2 * p->nbmax;
-  a.right_start = d.right_start; a.vals_out = d.vals_out; a.M = d.M;
+  a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out; a.M = d.M;
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt;
   return a;
 }
@@ -1396,7 +1457,8 @@ static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
   a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
   a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = 2 * p->nbmax;
   a.up_off = d.up_off; a.up = d.up; a.down_off = d.down_off; a.down = d.down;
-  a.right_start = d.right_start; a.vals_out = d.vals_out; a.row_base = d.row_base; a.rowcnt = d.rowcnt;
+  a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out;
+  a.row_base = d.row_base; a.rowcnt = d.rowcnt;
   a.lo_f = d.lo_f; a.seg_hi = d.seg_hi; a.seg_lo = d.seg_lo; a.hscan = d.hscan; a.rpos = d.rpos;
   a.rows = d.rows; a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.cs = d.cs;
   return a;
@@ -1438,6 +1500,13 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   p->S = in->n_samples;
   p->N = in->n_reads;
   p->Ng = in->n_reads_global > 0 ? in->n_reads_global : in->n_reads;
+  p->n_shards = in->n_shards > 0 ? in->n_shards : 1;
+  p->shard = in->shard;
+  if (p->shard < 0 || p->shard >= p->n_shards) { delete p; return fail(MPC_E_ARG, "shard out of range"); }
+  if (p->Ng < p->N || in->read_offset < 0 || in->read_offset + p->N > p->Ng) {
+    delete p;
+    return fail(MPC_E_ARG, "read shard [read_offset, read_offset + n_reads) outside [0, n_reads_global)");
+  }
   p->ref_len.assign(in->h_ref_len, in->h_ref_len + p->S);
   p->read_begin.assign(in->h_read_begin, in->h_read_begin + p->S + 1);
   p->h_n.resize(p->S);
@@ -1536,6 +1605,10 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_RLEN, Ng, 4);
   set(mpc_plan::B_RPOS, N > 0 ? N : 1, 4);
   set(mpc_plan::B_RSTART, G + 1, 4);
+  set(mpc_plan::B_RSLOC, G + 1, 4);
+  set(mpc_plan::B_ROFF, G + 1, 4);
+  set(mpc_plan::B_RCNT, G, 4);
+  set(mpc_plan::B_RCNTALL, G * p->n_shards, 4);
   set(mpc_plan::B_DIFF, G, 4);
   set(mpc_plan::B_SUB, G * 4, 4);
   set(mpc_plan::B_M, RU, 4);
@@ -1616,11 +1689,14 @@ int mpc_plan_buffer(const mpc_plan* p, int which, size_t* off, int64_t* count) {
     case MPC_BUF_MAXDEPTH: b = mpc_plan::B_MAXD; break;
     case MPC_BUF_ROWS: b = mpc_plan::B_ROWS; break;
     case MPC_BUF_ROWMETA: b = mpc_plan::B_META; break;
-    case MPC_BUF_RIGHT_KEY: b = mpc_plan::B_KIN; break;
-    case MPC_BUF_RIGHT_READ: b = mpc_plan::B_VIN; break;
+    case MPC_BUF_RIGHT_CNT: b = mpc_plan::B_RCNT; break;
+    case MPC_BUF_RIGHT_CNT_ALL: b = mpc_plan::B_RCNTALL; break;
     case MPC_BUF_HASLEFT: b = mpc_plan::B_HASLEFT; break;
     case MPC_BUF_MAXR: b = mpc_plan::B_MAXR; break;
     case MPC_BUF_RUN_M: b = mpc_plan::B_M; break;
+    case MPC_BUF_SEG_R: b = mpc_plan::B_SEGR; break;
+    case MPC_BUF_DIFF: b = mpc_plan::B_DIFF; break;
+    case MPC_BUF_SUB: b = mpc_plan::B_SUB; break;
     default: return fail(MPC_E_ARG, "unknown buffer");
   }
   *off = p->off[b];
@@ -1661,14 +1737,23 @@ int mpc_index(mpc_plan* p, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
   if (p->N > 0) hipLaunchKernelGGL(K_rsplit, dim3(nblk(p->N)), dim3(256), 0, st, d, p->sentinel);
-  if (p->Ng > 0) {
+  if (p->N > 0) {  // this shard's reads only: shards own contiguous read ranges
     size_t tb = p->cub_tmp;
     HIPCHK(hipcub::DeviceRadixSort::SortPairs(at<uint8_t>(p, mpc_plan::B_CUB), tb, d.keys_in, d.keys_out, d.vals_in,
-                                              d.vals_out, (int)p->Ng, 0, p->end_bit, st));
+                                              d.vals_out, (int)p->N, 0, p->end_bit, st));
   } else {
     HIPCHK(hipMemsetAsync(d.keys_out, 0xff, 4, st));
   }
-  hipLaunchKernelGGL(K_rstart, dim3(nblk(std::max<int64_t>(p->G + 1, p->Ng))), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(K_rstart, dim3(nblk(std::max<int64_t>(p->G + 1, p->N))), dim3(256), 0, st, d);
+  HIPCHK(hipGetLastError());
+  return MPC_OK;
+}
+
+int mpc_runs(mpc_plan* p, void* stream) {
+  NEED_BOUND(p);
+  hipStream_t st = (hipStream_t)stream;
+  Dev d = p->dev();
+  if (p->n_shards > 1) hipLaunchKernelGGL(K_runs, dim3(1), dim3(1024), 0, st, d);
   hipLaunchKernelGGL(K_zero_runs, dim3(nblk(p->runs_cap)), dim3(256), 0, st, d);
   HIPCHK(hipGetLastError());
   return MPC_OK;
@@ -1684,7 +1769,7 @@ int mpc_tally(mpc_plan* p, void* stream) {
   return MPC_OK;
 }
 
-int mpc_layout(mpc_plan* p, void* stream) {
+int mpc_segments(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
@@ -1694,8 +1779,17 @@ int mpc_layout(mpc_plan* p, void* stream) {
   size_t tb = p->cub_tmp;
   HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, d.hflag, d.hscan, (int)p->runs_cap, st));
   hipLaunchKernelGGL(K_seg_right, dim3(nblk(p->runs_cap)), dim3(256), 0, st, d);
+  HIPCHK(hipGetLastError());
+  return MPC_OK;
+}
+
+int mpc_layout(mpc_plan* p, void* stream) {
+  NEED_BOUND(p);
+  hipStream_t st = (hipStream_t)stream;
+  Dev d = p->dev();
+  uint8_t* tmp = at<uint8_t>(p, mpc_plan::B_CUB);
   hipLaunchKernelGGL(K_replay, dim3(nblk(p->G)), dim3(256), 0, st, d);
-  tb = p->cub_tmp;
+  size_t tb = p->cub_tmp;
   HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, d.rowcnt, d.row_base, (int)p->G, st));
   hipLaunchKernelGGL(K_rows_total, dim3(1), dim3(1), 0, st, d);
   HIPCHK(hipGetLastError());
@@ -1758,7 +1852,9 @@ int mpc_run(mpc_plan* p, double mdf, double gtf, void* stream) {
   int rc;
   if ((rc = mpc_parse(p, stream))) return rc;
   if ((rc = mpc_index(p, stream))) return rc;
+  if ((rc = mpc_runs(p, stream))) return rc;
   if ((rc = mpc_tally(p, stream))) return rc;
+  if ((rc = mpc_segments(p, stream))) return rc;
   if ((rc = mpc_layout(p, stream))) return rc;
   if ((rc = mpc_rows(p, stream))) return rc;
   return mpc_consensus(p, mdf, gtf, stream);

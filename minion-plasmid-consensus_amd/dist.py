@@ -1,0 +1,231 @@
+"""Multi-GPU pileup: reads sharded across GPUs, one global pileup.
+
+Shards own CONTIGUOUS global read ranges in shard order (rank k holds the
+k-th block of every sample's reads).  This preserves the one piece of the
+reference that depends on read order: the slot layout at gaps that receive
+both LEFT and RIGHT strings (processBaseString_leftIndel / _rightIndel,
+mapped_paf_read_parser.py:37-72, driven in PAF first-occurrence order :292).
+Everything else is an order-free integer tally.  See SURVEY.md 8(e).
+
+Every shard runs the phases of include/mpc.h on its own reads.  Between the
+phases it exchanges small arrays (no read data moves):
+
+    after parse     OR   hasleft bitmap           (which gaps hold LEFT events)
+                    SUM  diff, sub                (depth / substitution tallies)
+    after index     GATHER per-gap mixed RIGHT counts -> global run index space
+                    MAX  maxR                     (RIGHT-only gaps)
+    after tally     MAX  M per run                (longest LEFT string per run)
+    after segments  MAX  segR per segment         (longest RIGHT string per segment)
+    after rows      SUM  rows                     (odd rows from shard 0, slot tallies from all)
+
+after which layout and consensus are identical on every shard.  The protocol
+is written once against an ``Exchange``: ``DistExchange`` is one shard per
+process over torch.distributed (RCCL over xGMI on GPUs; gloo in the CPU
+tests), ``LocalExchange`` drives several shards in one process (used by the
+GPU parity test to check the sharded kernels bit-exactly against one GPU).
+"""
+import numpy as np
+
+from . import engine as eng
+
+
+class LocalExchange:
+    """Collectives over a list of tensors that all live in this process (one per shard)."""
+
+    def reduce(self, ts, op):
+        acc = ts[0].clone()
+        for t in ts[1:]:
+            t = t.to(acc.device)
+            if op == "sum":
+                acc += t
+            elif op == "max":
+                acc = acc.maximum(t)
+            elif op == "or":
+                acc |= t
+            else:
+                raise ValueError(op)
+        for t in ts:
+            t.copy_(acc.to(t.device))
+
+    def gather(self, ts, outs):
+        """outs[i] (shape [n_shards * k]) <- concatenation of ts in shard order."""
+        import torch
+        for o in outs:
+            o.copy_(torch.cat([t.to(o.device) for t in ts]))
+
+    def max_int(self, xs):
+        return [max(xs)] * len(xs)
+
+    def sizes(self, ns):
+        return list(ns)
+
+
+class DistExchange:
+    """One shard per process over a torch.distributed process group."""
+
+    def __init__(self, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group)
+        self.rank = dist.get_rank(group)
+
+    def reduce(self, ts, op):
+        (t,) = ts
+        d = self.dist
+        if op == "sum":
+            d.all_reduce(t, op=d.ReduceOp.SUM, group=self.group)
+        elif op == "max":
+            d.all_reduce(t, op=d.ReduceOp.MAX, group=self.group)
+        elif op == "or":
+            # RCCL has no bitwise reduction: gather the bitmaps and OR them
+            import torch
+            parts = [torch.empty_like(t) for _ in range(self.world)]
+            d.all_gather(parts, t, group=self.group)
+            acc = parts[0].clone()
+            for x in parts[1:]:
+                acc |= x
+            t.copy_(acc)
+        else:
+            raise ValueError(op)
+
+    def gather(self, ts, outs):
+        (t,), (o,) = ts, outs
+        import torch
+        parts = list(o.view(self.world, -1).unbind(0))
+        tmp = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(tmp, t, group=self.group)
+        for p, x in zip(parts, tmp):
+            p.copy_(x)
+
+    def _ints(self, xs, op):
+        import torch
+        dev = "cuda" if self.dist.get_backend(self.group) == "nccl" else "cpu"
+        if op == "max":
+            t = torch.tensor(xs, dtype=torch.int64, device=dev)
+            self.dist.all_reduce(t, op=self.dist.ReduceOp.MAX, group=self.group)
+            return [int(t.item())]
+        t = torch.tensor(xs, dtype=torch.int64, device=dev)
+        parts = [torch.empty_like(t) for _ in range(self.world)]
+        self.dist.all_gather(parts, t, group=self.group)
+        return [int(p.item()) for p in parts]
+
+    def max_int(self, xs):
+        return self._ints(xs, "max")
+
+    def sizes(self, ns):
+        return self._ints(ns, "gather")
+
+
+def split_samples(samples, n_shards):
+    """Per-shard sample lists: shard k gets the k-th contiguous block of every
+    sample's reads (buffers are shared, offsets sliced)."""
+    out = [[] for _ in range(n_shards)]
+    for s in samples:
+        n = len(s["tstart"])
+        cuts = [n * k // n_shards for k in range(n_shards + 1)]
+        for k in range(n_shards):
+            a, b = cuts[k], cuts[k + 1]
+            part = dict(s)
+            for key in ("cs_off", "up_off", "down_off"):
+                part[key] = np.asarray(s[key])[a: b + 1]
+            for key in ("tstart", "aligned", "tend"):
+                if key in s:
+                    part[key] = np.asarray(s[key])[a:b]
+            out[k].append(part)
+    return out
+
+
+def shard_layout(n_reads_per_shard):
+    """(read_offset, n_reads_global) of every shard: shards are contiguous, in order."""
+    offs = np.concatenate([[0], np.cumsum(n_reads_per_shard)]).astype(np.int64)
+    return [int(o) for o in offs[:-1]], int(offs[-1])
+
+
+def exchange_step(plans, ex, mdf, gtf, stream=None):
+    """One global pileup over the shards in ``plans`` (all of this process's
+    shards; with DistExchange exactly one).  Collective: every shard must call it."""
+    import torch
+    i32 = torch.int32
+
+    def each(phase, *args):
+        for p in plans:
+            p.phase(phase, stream, *args)
+
+    each("parse")
+    ex.reduce([p.buffer(eng.BUF_HASLEFT, i32) for p in plans], "or")
+    ex.reduce([p.buffer(eng.BUF_DIFF, i32) for p in plans], "sum")
+    ex.reduce([p.buffer(eng.BUF_SUB, i32) for p in plans], "sum")
+    each("index")
+    ex.gather([p.buffer(eng.BUF_RIGHT_CNT, i32) for p in plans], [p.buffer(eng.BUF_RIGHT_CNT_ALL, i32) for p in plans])
+    ex.reduce([p.buffer(eng.BUF_MAXR, i32) for p in plans], "max")
+    each("runs")
+    each("tally")
+    ex.reduce([p.buffer(eng.BUF_RUN_M, i32) for p in plans], "max")
+    each("segments")
+    ex.reduce([p.buffer(eng.BUF_SEG_R, i32) for p in plans], "max")
+    each("layout")
+    each("rows")
+    ex.reduce([p.buffer(eng.BUF_ROWS, i32) for p in plans], "sum")
+    each("consensus", mdf, gtf)
+
+
+class ShardedPileup:
+    """Shards of one global pileup.  ``shards`` is a list of per-shard sample
+    lists (every shard holds the same samples, i.e. the same references, and
+    its own contiguous block of each sample's reads).
+
+    With ``ex=None`` all shards live in this process (LocalExchange); with a
+    DistExchange this process holds exactly one shard (``rank`` of the group).
+    """
+
+    def __init__(self, shards, devices, ex=None, row_cap=None):
+        self.ex = ex or LocalExchange()
+        local = len(shards)
+        if isinstance(self.ex, DistExchange):
+            assert local == 1, "one shard per process"
+            ranks = [self.ex.rank]
+            n_shards = self.ex.world
+        else:
+            ranks = list(range(local))
+            n_shards = local
+        n_local = [sum(len(s["tstart"]) for s in smp) for smp in shards]
+        n_all = self.ex.sizes(n_local)
+        offs, ng = shard_layout(n_all)
+        self.batches = [eng.Batch(smp, device=dev, read_offset=offs[r], n_reads_global=ng, shard=r,
+                                  n_shards=n_shards) for smp, dev, r in zip(shards, devices, ranks)]
+        cap = row_cap or max(b.row_estimate() for b in self.batches)
+        cap = self.ex.max_int([cap] * local)[0] if isinstance(self.ex, DistExchange) else cap
+        self.plans = [eng.Plan(b, cap) for b in self.batches]
+        self._sized = False
+
+    # bench.py interface (one local shard)
+    @property
+    def batch(self):
+        return self.batches[0]
+
+    @property
+    def plan(self):
+        return self.plans[0]
+
+    def step(self, mdf, gtf, stream=None):
+        exchange_step(self.plans, self.ex, mdf, gtf, stream)
+        if not self._sized:
+            # the layout (and so the row count) is identical on every shard
+            st = self.plans[0].status()
+            flags = int(st[eng.MPC_ST_FLAGS])
+            flags = self.ex.max_int([flags] * len(self.plans))[0] if isinstance(self.ex, DistExchange) else flags
+            if flags & eng.DE_CAPACITY:
+                need = int(st[eng.MPC_ST_ROWS_NEEDED]) + 16
+                self.plans = [eng.Plan(b, need) for b in self.batches]
+                exchange_step(self.plans, self.ex, mdf, gtf, stream)
+            self._sized = True
+
+    def check(self):
+        for p in self.plans:
+            st = p.status()
+            if int(st[eng.MPC_ST_FLAGS]):
+                raise eng.DataError(int(st[eng.MPC_ST_FLAGS]), int(st[eng.MPC_ST_FIRST_READ]))
+
+    def fetch(self):
+        return self.plans[0].fetch()

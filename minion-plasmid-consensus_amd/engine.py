@@ -14,10 +14,12 @@ from . import _build
 
 LIB_PATH = _build.LIBMPC
 
+ABI_VERSION = 2
 MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED = 0, 1, 2, 3
 DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL = 1, 2, 4, 8, 16, 32
-(BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_KEY, BUF_RIGHT_READ,
- BUF_HASLEFT, BUF_MAXR, BUF_RUN_M) = range(11)
+(BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_CNT, BUF_RIGHT_CNT_ALL,
+ BUF_HASLEFT, BUF_MAXR, BUF_RUN_M, BUF_SEG_R, BUF_DIFF, BUF_SUB) = range(14)
+PHASES = ("parse", "index", "runs", "tally", "segments", "layout", "rows")
 
 DE_NAMES = {DE_OP: "Unknown operator", DE_VALUE: "ValueError", DE_INDEX: "IndexError", DE_KEY: "KeyError",
             DE_CAPACITY: "row capacity", DE_INTERNAL: "internal invariant"}
@@ -56,6 +58,8 @@ class _Input(ctypes.Structure):
         ("cs_base", ctypes.c_int64),
         ("read_offset", ctypes.c_int64),
         ("n_reads_global", ctypes.c_int64),
+        ("shard", ctypes.c_int32),
+        ("n_shards", ctypes.c_int32),
     ]
 
 
@@ -77,16 +81,17 @@ def lib():
         L.mpc_plan_bind.argtypes = [vp, vp, ctypes.c_size_t]
         L.mpc_plan_buffer.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(i64)]
         L.mpc_plan_set_input.argtypes = [vp, ctypes.POINTER(_Input)]
-        for f in ("mpc_parse", "mpc_index", "mpc_tally", "mpc_layout", "mpc_rows"):
-            getattr(L, f).argtypes = [vp, vp]
+        for f in PHASES:
+            getattr(L, "mpc_" + f).argtypes = [vp, vp]
         L.mpc_consensus.argtypes = [vp, dbl, dbl, vp]
         L.mpc_run.argtypes = [vp, dbl, dbl, vp]
         L.mpc_profile_kernel.argtypes = [vp, i32, vp]
         L.mpc_profile_kernel.restype = i32
         for f in ("mpc_plan_create", "mpc_plan_destroy", "mpc_plan_workspace_bytes", "mpc_plan_bind",
-                  "mpc_plan_buffer", "mpc_plan_set_input", "mpc_parse", "mpc_index", "mpc_tally",
-                  "mpc_layout", "mpc_rows", "mpc_consensus", "mpc_run"):
+                  "mpc_plan_buffer", "mpc_plan_set_input", "mpc_consensus", "mpc_run") + tuple("mpc_" + x for x in PHASES):
             getattr(L, f).restype = i32
+        if L.mpc_version() != ABI_VERSION:
+            raise MpcError(f"{LIB_PATH}: ABI {L.mpc_version()} != {ABI_VERSION} (rebuild)")
         _lib = L
     return _lib
 
@@ -105,7 +110,7 @@ class Batch:
     """Device-resident inputs of one launch: one or more samples (strands /
     plasmids) concatenated, reads grouped by sample."""
 
-    def __init__(self, samples, device=0, read_offset=0, n_reads_global=None):
+    def __init__(self, samples, device=0, read_offset=0, n_reads_global=None, shard=0, n_shards=1):
         torch = _torch()
         if not torch.cuda.is_available():
             raise MpcError("no HIP device visible (the pileup path has no CPU fallback)")
@@ -118,6 +123,7 @@ class Batch:
         self.n_reads = int(self.read_begin[-1])
         self.read_offset = int(read_offset)
         self.n_reads_global = int(n_reads_global if n_reads_global is not None else self.n_reads)
+        self.shard, self.n_shards = int(shard), int(n_shards)
 
         def cat_bytes(key, offkey):
             bufs, offs, base = [], [], 0
@@ -174,6 +180,7 @@ class Batch:
             h_read_begin=self._keep[1].ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
             n_reads=self.n_reads, cs_bytes=self.cs_bytes, cs_base=0,
             read_offset=self.read_offset, n_reads_global=self.n_reads_global,
+            shard=self.shard, n_shards=self.n_shards,
         )
 
     def row_estimate(self):

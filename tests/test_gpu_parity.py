@@ -111,3 +111,24 @@ def test_many_samples_one_launch(pkg):
     res = pkg.engine.pileup(samples, 0.1, 5.0)
     for k, (s, r) in enumerate(zip(samples, res)):
         _cmp(r, _oracle(s, 0.1, 5.0), ("multi", k))
+
+
+SHARDED = [(SYNTH[0], 2), (SYNTH[1], 3), (SYNTH[2], 2), (SYNTH[3], 3), (SYNTH[4], 4), (SYNTH[5], 2)]
+
+
+@pytest.mark.parametrize("spec,n_shards", SHARDED,
+                         ids=lambda x: f"{x}" if isinstance(x, int) else f"n{x['n']}_{x['profile']}_s{x['seed']}")
+def test_sharded_matches_oracle(pkg, spec, n_shards):
+    """Reads split into contiguous shards (multi-GPU protocol of dist.py, all
+    shards on this GPU, exchanges in-process): every shard ends with the
+    single-pileup result, bit-exact."""
+    dist = importlib.import_module("minion-plasmid-consensus_amd.dist")
+    syn = pkg.synth.Synth(**spec)
+    samples = [syn.sample(0), syn.sample(1)]
+    sp = dist.ShardedPileup(dist.split_samples(samples, n_shards), [0] * n_shards)
+    for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
+        sp.step(mdf, gtf)
+        exp = [_oracle(s, mdf, gtf) for s in samples]
+        for k, plan in enumerate(sp.plans):
+            for s, (r, e) in enumerate(zip(plan.fetch(), exp)):
+                _cmp(r, e, ("shard", k, s, mdf))

@@ -11,7 +11,8 @@
  *   Step 4 cs tokenizer + processOperation :285-323, :74-104
  *                                                  mpc_parse()           (K_parse)
  *   processBaseString_leftIndel/rightIndel :37-72  mpc_index() .. mpc_rows()
- *                                                  (even-slot layout, tallies)
+ *                                                  (even-slot layout, tallies: K_rsplit, K_left,
+ *                                                  K_replay, K_ins, K_flank)
  *   Step 5 max depth :332-341                      mpc_consensus()       (K_consensus)
  *   Step 6 consensus/threshold :348-439            mpc_consensus()       (K_consensus, K_emit)
  *   whole Step 4-6                                 mpc_run()
@@ -39,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MPC_ABI_VERSION 2
+#define MPC_ABI_VERSION 3
 
 /* return codes */
 #define MPC_OK 0
@@ -113,7 +114,7 @@ enum {
   MPC_BUF_HASLEFT,      /* uint32[(gaps+31)/32 + 1] bitmap: gap holds a LEFT event (exchange: OR)         */
   MPC_BUF_MAXR,         /* int32[gaps] longest RIGHT event at RIGHT-only gaps       (exchange: MAX)        */
   MPC_BUF_RUN_M,        /* int32[n_reads_global + gaps] longest LEFT event per run  (exchange: MAX)        */
-  MPC_BUF_SEG_R,        /* int32[n_reads_global + gaps] longest RIGHT event per segment (exchange: MAX)    */
+  MPC_BUF_RUN_R,        /* int32[n_reads_global + gaps] length of the RIGHT event closing each run (exchange: MAX) */
   MPC_BUF_DIFF,         /* int32[gaps] read-span/deletion difference array          (exchange: SUM)        */
   MPC_BUF_SUB,          /* uint32[gaps][4] substitution tallies                     (exchange: SUM)        */
   MPC_BUF_COUNT
@@ -136,21 +137,19 @@ int mpc_plan_set_input(mpc_plan* plan, const mpc_input* in);
 
 /* Phases (single GPU: mpc_run() = all of them, in this order).  With
  * n_shards > 1 the host inserts these collectives (Multi-GPU):
- *   mpc_parse    ; OR  HASLEFT, SUM DIFF/SUB (may be deferred to before rows)
+ *   mpc_parse    ; OR  HASLEFT, SUM DIFF/SUB (may be deferred to before layout)
  *   mpc_index    ; ALL-GATHER RIGHT_CNT -> RIGHT_CNT_ALL, MAX MAXR
- *   mpc_runs     (global run index space)
- *   mpc_tally    ; MAX RUN_M
- *   mpc_segments ; MAX SEG_R
+ *   mpc_runs     (global run index space, RIGHT length per run)
+ *   mpc_tally    ; MAX RUN_M, MAX RUN_R
  *   mpc_layout   (identical on every shard)
  *   mpc_rows     ; SUM ROWS  (odd rows come from shard 0, others add flank / insertion bases)
  *   mpc_consensus (identical on every shard) */
-int mpc_parse(mpc_plan* plan, void* stream);        /* cs -> events, i_end, LEFT marks, tallies  */
-int mpc_index(mpc_plan* plan, void* stream);        /* mixed downstream keys, stable sort        */
-int mpc_runs(mpc_plan* plan, void* stream);         /* global run index space, clear run maxima  */
-int mpc_tally(mpc_plan* plan, void* stream);        /* work units, run M                         */
-int mpc_segments(mpc_plan* plan, void* stream);     /* segments, RIGHT maxima per segment        */
-int mpc_layout(mpc_plan* plan, void* stream);       /* even-slot replay, row offsets             */
-int mpc_rows(mpc_plan* plan, void* stream);         /* depth, odd rows, slot (flank/ins) tallies */
+int mpc_parse(mpc_plan* plan, void* stream);        /* clear; cs -> i_end, LEFT gap bits, tallies, insertion events */
+int mpc_index(mpc_plan* plan, void* stream);        /* downstream (RIGHT) events at mixed gaps, stable (gap, read) sort */
+int mpc_runs(mpc_plan* plan, void* stream);         /* shards > 1: global run index space            */
+int mpc_tally(mpc_plan* plan, void* stream);        /* work units; longest LEFT string per run (M)   */
+int mpc_layout(mpc_plan* plan, void* stream);       /* per-gap replay of the slot layout, row counts */
+int mpc_rows(mpc_plan* plan, void* stream);         /* row offsets, depth, odd rows, insertion and flank tallies */
 int mpc_consensus(mpc_plan* plan, double min_depth_factor, double global_threshold_factor,
                   void* stream);                    /* max depth, calls, compaction            */
 int mpc_run(mpc_plan* plan, double min_depth_factor, double global_threshold_factor, void* stream);
@@ -162,6 +161,7 @@ int mpc_run(mpc_plan* plan, double min_depth_factor, double global_threshold_fac
 #define MPC_K_PARSE 0
 #define MPC_K_LEFT 2
 #define MPC_K_FLANK 3
+#define MPC_K_INS 4
 int mpc_profile_kernel(mpc_plan* plan, int which, void* stream);
 
 #ifdef __cplusplus

@@ -158,6 +158,23 @@ __device__ __forceinline__ void peel_atomic_add(int32_t* base, int64_t key, int3
   }
 }
 
+// Block-aggregated atomicMax for keys that repeat across a whole block (hot
+// gaps: thousands of reads start at gap 0 / end at gap n).  Same-address global
+// atomics serialize at the memory side (~12 ns each), so the block's first
+// thread's key is reduced in LDS and flushed with ONE atomic; other keys go
+// through the wave-aggregated path.  Every thread of the block must call it.
+__device__ __forceinline__ void block_atomic_max(int32_t* base, int64_t key, int32_t val, bool active,
+                                                 int64_t* s_key, int32_t* s_val) {
+  __syncthreads();
+  if (threadIdx.x == 0) { *s_key = active ? key : -1; *s_val = INT32_MIN; }
+  __syncthreads();
+  const bool mine = active && key == *s_key;
+  if (mine) atomicMax(s_val, val);
+  peel_atomic_max(base, key, val, active && !mine);
+  __syncthreads();
+  if (threadIdx.x == 0 && *s_key >= 0 && *s_val != INT32_MIN) atomicMax(base + *s_key, *s_val);
+}
+
 // number of entries < x in sorted a[lo, hi)
 __device__ __forceinline__ int64_t lower_bound_i32(const int32_t* a, int64_t lo, int64_t hi, int32_t x) {
   while (lo < hi) {

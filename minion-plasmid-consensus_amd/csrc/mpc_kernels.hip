@@ -22,7 +22,6 @@
 //   consensus K_call        per-slot top/second/tie/N (:363-439), max depth
 //             scan, K_emit  threshold test + ordered compaction of the calls
 #include <hip/hip_runtime.h>
-#include <hipcub/hipcub.hpp>
 
 #include <algorithm>
 #include <cstdio>
@@ -88,6 +87,7 @@ struct Dev {  // device-side views of the plan for the small kernels (passed by 
   uint32_t* hasleft;                 // bitmap over gaps
   int32_t* maxR;
   uint32_t* keys_in; int32_t* vals_in; uint32_t* keys_out; int32_t* vals_out;
+  uint32_t* keys_tmp; int32_t* vals_tmp; int32_t* bcnt; int32_t* bpre;  // K_rsplit -> K_rsort
   int32_t* rlen;                     // [Ng] downstream length by global read
   int32_t* rpos;                     // [N] local read -> position of its mixed RIGHT event in the sorted list
   int32_t* right_start;              // [G+1] mixed RIGHT events (all shards) with gap < g
@@ -98,12 +98,13 @@ struct Dev {  // device-side views of the plan for the small kernels (passed by 
   int32_t shard, n_shards;
   int32_t* diff;                     // [G]
   uint32_t* sub;                     // [G][4]
-  int32_t* M;                        // [Ng+G] per run
-  int32_t* hflag; int32_t* hscan; int32_t* segR; int32_t* seg_lo; int32_t* seg_hi; int32_t* seg_run;
+  int32_t* M;                        // [Ng+G] per run: longest LEFT string
+  int32_t* runR;                     // [Ng+G] per run: length of the RIGHT string closing it
+  int32_t* hiR; int32_t* loR;        // [Ng+G] per run: hi seen by its LEFT events, lo seen by its RIGHT event
   int32_t* lo_f; int32_t* rowcnt; int32_t* row_base;
-  int32_t* depth;
+  int32_t* bsum;                     // [2 * ceil(G / kGB)] block sums of rowcnt, diff
   uint32_t* rows; uint8_t* meta; int64_t row_cap;
-  uint32_t* res; int32_t* keep; int32_t* keep_scan; uint32_t* calls; int32_t* ncalls; uint32_t* maxdepth;
+  uint32_t* res; int32_t* keep; int32_t* ksum; uint32_t* calls; int32_t* ncalls; uint32_t* maxdepth;
   double mdf, gtf;
 };
 
@@ -293,8 +294,22 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
 // (LDS), insertion events (per-wave LDS ring), LEFT-gap bits (LDS bitmap); no
 // global store inside the rounds.  Epilogue: flush tallies, bucket-sort
 // insertion events by gap.
+#ifdef MPC_PROF_PARSE
+// instrumentation build only: per-section shader cycles of K_parse summed over waves
+__device__ unsigned long long g_prof[16];
+#define PROF_T(x) const unsigned long long x = __builtin_amdgcn_s_memtime()
+#define PROF_ADD(k, v) pr[k] += (v)
+#else
+#define PROF_T(x)
+#define PROF_ADD(k, v)
+#endif
+
 template <bool FUSED>
 __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
+#ifdef MPC_PROF_PARSE
+  unsigned long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  PROF_T(tk0);
+#endif
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int l = lane();
   const int w = uniform_i32((int)(threadIdx.x >> 6));
@@ -347,6 +362,7 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   bool carry = false;       // slot 0 holds a read continuing into this window
   WinIn cur = fetch_window(a, P, rs0, l);
   while (P < wend) {
+    PROF_T(tw0);
     const int64_t A = P & ~(int64_t)15;
     // ---- window end: at most 63 read starts in [P, E) ----
     int64_t E = A + kWin < wend ? A + kWin : wend;
@@ -396,11 +412,7 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       W.s_read[q] = (int32_t)(rs0 + l);
       W.s_iend[q] = (ts < 0 ? 0 : (ts > n ? n + 1 : ts)) | (dn > 0 ? 1 << 30 : 0);
     }
-    {  // upstream flank = LEFT event at gap tstart
-      const uint64_t bl = ballot(lflank);
-      if (lflank) W.ibuf[nib + lanes_below(bl)] = flank_event(cur.ts, false, a.read_offset + rs0 + l);
-      nib += __popcll(bl);
-    }
+    (void)lflank;  // upstream flank = LEFT event at gap tstart: only its gap bit (tallied per read later)
     wave_sync_lds();
     {  // read-start bits of every known start in the stage
       const int64_t rel = cur.o - A;
@@ -409,6 +421,7 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
         atomicOr(reinterpret_cast<uint32_t*>(W.ra) + (rel >> 5), 1u << (rel & 31));
       }
     }
+    PROF_T(tw1);
     // ---- prefetch the next window ----
     const int64_t Pn = E, rsn = rs0 + nst;
     WinIn nxt;
@@ -462,6 +475,7 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
     }
     wave_sync_lds();
 
+    PROF_T(tw2);
     // ---- rounds: one token per lane ----
     int64_t G = 0;  // advances of the window's earlier rounds
     int qc = 0;     // read starts of the window's earlier rounds
@@ -556,13 +570,10 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       if (ins_inline)
         W.ibuf[nib + lanes_below(bins)] = te == 0 ? ins_event(itok, olen, pay, a.read_offset + rl)
                                                  : ins_event((int)kNullGap, 1, 0u, a.read_offset + rl);
-      bool rflank = false;
-      int ie = 0;
       if (last) {  // the read's last operation: i_end, downstream check, span
         const int64_t ia = i64 + adv;
-        ie = (int)(ia < 0 ? 0 : (ia > n ? n + 1 : ia));
+        const int ie = (int)(ia < 0 ? 0 : (ia > n ? n + 1 : ia));
         const int dnf = W.s_iend[q] & (1 << 30);
-        rflank = dnf && ie <= n;  // downstream flank = RIGHT event at gap i_end
         if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
         W.s_iend[q] = ie | dnf;
         const int ts = W.s_ts[q];
@@ -573,14 +584,10 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       G += atot;
       qc += __popcll(brs);
       nib += __popcll(bins);
-      const uint64_t brf = ballot(rflank);
-      if (brf) {
-        if (nib + 64 > kIB) flush_ibuf();
-        if (rflank) W.ibuf[nib + lanes_below(brf)] = flank_event(ie, true, a.read_offset + rl);
-        nib += __popcll(brf);
-      }
     }
     wave_sync_lds();
+    PROF_T(tw3);
+    PROF_ADD(0, tw1 - tw0); PROF_ADD(1, tw2 - tw1); PROF_ADD(2, tw3 - tw2); PROF_ADD(4, 1); PROF_ADD(5, (T + 63) / 64);
     // ---- reads that ended in this window: i_end; carry the open one ----
     if (l <= nst && (l > 0 || carry) && W.s_end[l] <= E) a.i_end[W.s_read[l]] = W.s_iend[l] & ~(1 << 30);
     const bool cont = (nst > 0 || carry) && W.s_end[nst] > E;
@@ -596,6 +603,9 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
     wave_sync_lds();
     P = Pn;
     rs0 = rsn;
+#ifdef MPC_PROF_PARSE
+    { PROF_T(tw4); PROF_ADD(3, tw4 - tw3); }
+#endif
     if (Pn < wend) cur = nxt;
   }
   // reads starting at the range end have an empty cs
@@ -605,9 +615,20 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
     a.i_end[r] = ts < 0 ? 0 : (ts > n ? n + 1 : ts);
   }
   if (nib) flush_ibuf();
+#ifdef MPC_PROF_PARSE
+  {
+    PROF_T(tk1);
+    PROF_ADD(6, tk1 - tk0);
+    if (l == 0) for (int k = 0; k < 8; ++k) atomicAdd(&g_prof[k], pr[k]);
+  }
+#endif
   __syncthreads();
   // ---- flush LDS tallies and the LEFT-gap bitmap ----
+#ifdef MPC_EXP_NOFLUSH_PARSE
+  if (false) {
+#else
   if (fused) {
+#endif
     for (int p = threadIdx.x; p <= n; p += blockDim.x) {
       const int32_t dv = diff_l[p];
       if (dv) atomicAdd(a.diff + gb + p, dv);
@@ -627,10 +648,9 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
     if (g0 & 31) atomicOr(a.hasleft + (g0 >> 5) + 1, v >> (32 - (g0 & 31)));
   }
   __syncthreads();
-  // ---- bucket-sort this workgroup's events by gap (counting sort): insertion
-  //      buckets [0, nbk), flank buckets [nbk, 2 nbk) ----
+  // ---- bucket-sort this workgroup's insertion events by gap (counting sort) ----
   const int nbk = (n + 1 + kBW - 1) / kBW;
-  const int nbt = 2 * nbk;
+  const int nbt = nbk;
   uint32_t* bcnt = reinterpret_cast<uint32_t*>(uni);  // aliases the (flushed) tallies
   uint32_t* bcur = bcnt + nbt;
   const int Ev = (int)misc[0];
@@ -639,7 +659,7 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
     const uint64_t ev = a.ins_raw[rb_wg + k];
     const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
-    if (gap <= (uint32_t)n) atomicAdd(bcnt + gap / kBW + ((ev & kFlankBit) ? nbk : 0), 1u);
+    if (gap <= (uint32_t)n) atomicAdd(bcnt + gap / kBW, 1u);
   }
   __syncthreads();
   if (threadIdx.x < 64) {  // exclusive scan over buckets by one wave
@@ -661,7 +681,7 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
     const uint64_t ev = a.ins_raw[rb_wg + k];
     const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
-    if (gap <= (uint32_t)n) a.ins_sorted[rb_wg + atomicAdd(bcur + gap / kBW + ((ev & kFlankBit) ? nbk : 0), 1u)] = ev;
+    if (gap <= (uint32_t)n) a.ins_sorted[rb_wg + atomicAdd(bcur + gap / kBW, 1u)] = ev;
   }
 }
 
@@ -672,12 +692,16 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool has_left(const uint32_t* bm, int64_t g) { return (bm[g >> 5] >> (g & 31)) & 1u; }
 
-__global__ __launch_bounds__(256) void K_rsplit(Dev d, uint32_t sentinel) {
+__global__ __launch_bounds__(1024) void K_rsplit(Dev d) {
+  __shared__ int64_t s_key;
+  __shared__ int32_t s_val;
+  __shared__ int32_t s_w[16];
   const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
   const bool in = r < d.N;
   int64_t g = -1;
   int32_t len = 0;
   bool mixed = false;
+  const int64_t rg = d.read_offset + r;
   if (in) {
     const int s = d.sample[r];
     const int64_t n = d.n_of[s];
@@ -688,36 +712,151 @@ __global__ __launch_bounds__(256) void K_rsplit(Dev d, uint32_t sentinel) {
       g = d.gbase[s] + ie;
       mixed = has_left(d.hasleft, g);
     }
-    const int64_t rg = d.read_offset + r;
-    d.keys_in[r] = mixed ? (uint32_t)g : sentinel;
-    d.vals_in[r] = (int32_t)rg;
     d.rlen[rg] = len;
   }
-  peel_atomic_max(d.maxR, g < 0 ? 0 : g, len, in && g >= 0 && !mixed);
+  // block-local stable compaction of the mixed events (read order), for K_rsort
+  const int f = mixed ? 1 : 0;
+  const int inc = wave_scan_i32(f);
+  const int w = threadIdx.x >> 6;
+  if (lane() == 63) s_w[w] = inc;
+  __syncthreads();
+  int wpre = 0;
+  for (int k = 0; k < w; ++k) wpre += s_w[k];
+  if (mixed) {
+    const int64_t o = (int64_t)blockIdx.x * blockDim.x + wpre + inc - 1;
+    d.keys_in[o] = (uint32_t)g;
+    d.vals_in[o] = (int32_t)rg;
+  }
+  if (threadIdx.x == blockDim.x - 1) d.bcnt[blockIdx.x] = wpre + inc;
+  block_atomic_max(d.maxR, g < 0 ? 0 : g, len, in && g >= 0 && !mixed, &s_key, &s_val);
+}
+
+// ---------------------------------------------------------------------------
+// K_rsort: the mixed RIGHT events (partial reads ending at gaps that also hold
+// LEFT events: few) sorted by (gap, read).  One workgroup: gather the per-block
+// lists of K_rsplit (in read order), then a stable LSD radix sort on the gap
+// (8-bit digits, wave multi-split ranks) -- in LDS when the list fits, else
+// ping-ponging through HBM (same code, generic pointers).
+// ---------------------------------------------------------------------------
+constexpr int kRS = 1024;
+constexpr int kSortLds = 8192;
+
+__global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t end_bit) {
+  __shared__ uint32_t lk[2][kSortLds];
+  __shared__ int32_t lv[2][kSortLds];
+  __shared__ int32_t wc[kRS / 64][256];
+  __shared__ int32_t hb[256];
+  __shared__ int32_t s_w[kRS / 64];
+  __shared__ int32_t s_carry;
+  const int tid = threadIdx.x, l = lane(), w = tid >> 6;
+  // exclusive prefix of the per-block counts -> bpre[0..nblocks]
+  if (tid == 0) s_carry = 0;
+  __syncthreads();
+  for (int c0 = 0; c0 < nblocks; c0 += kRS) {
+    const int b = c0 + tid;
+    const int v = b < nblocks ? d.bcnt[b] : 0;
+    const int inc = wave_scan_i32(v);
+    if (l == 63) s_w[w] = inc;
+    __syncthreads();
+    int pre = s_carry;
+    for (int k = 0; k < w; ++k) pre += s_w[k];
+    if (b < nblocks) d.bpre[b] = pre + inc - v;
+    __syncthreads();
+    if (tid == kRS - 1) s_carry = pre + inc;
+    __syncthreads();
+  }
+  const int64_t M = s_carry;
+  if (tid == 0) { d.bpre[nblocks] = (int32_t)M; d.status[MPC_ST_MIXED] = (uint32_t)M; }
+  if (M == 0) return;
+  const int passes = (end_bit + 7) / 8;
+  const bool in_lds = M <= kSortLds;
+  uint32_t* kb[2];
+  int32_t* vb[2];
+  if (in_lds) { kb[0] = lk[0]; kb[1] = lk[1]; vb[0] = lv[0]; vb[1] = lv[1]; }
+  else {
+    kb[passes & 1] = d.keys_out; vb[passes & 1] = d.vals_out;
+    kb[(passes + 1) & 1] = d.keys_tmp; vb[(passes + 1) & 1] = d.vals_tmp;
+  }
+  __syncthreads();
+  // gather (read order) into buffer 0
+  for (int64_t i = tid; i < M; i += kRS) {
+    int lo = 0, hi = nblocks - 1;  // last block with bpre <= i
+    while (lo < hi) {
+      const int mid = (lo + hi + 1) >> 1;
+      if (d.bpre[mid] <= i) lo = mid; else hi = mid - 1;
+    }
+    const int64_t src = (int64_t)lo * kRS + (i - d.bpre[lo]);
+    kb[0][i] = d.keys_in[src];
+    vb[0][i] = d.vals_in[src];
+  }
+  __syncthreads();
+  const uint64_t lt = (1ull << l) - 1ull;
+  for (int p = 0; p < passes; ++p) {
+    const int sh = 8 * p;
+    const uint32_t* sk = kb[p & 1];
+    const int32_t* sv = vb[p & 1];
+    uint32_t* dk = (in_lds && p == passes - 1) ? d.keys_out : kb[(p + 1) & 1];
+    int32_t* dv = (in_lds && p == passes - 1) ? d.vals_out : vb[(p + 1) & 1];
+    if (tid < 256) hb[tid] = 0;
+    __syncthreads();
+    for (int64_t i = tid; i < M; i += kRS) atomicAdd(&hb[(sk[i] >> sh) & 255u], 1);
+    __syncthreads();
+    if (tid < 64) {  // exclusive scan of the 256 digit counts (4 per lane)
+      const int x0 = hb[4 * tid], x1 = hb[4 * tid + 1], x2 = hb[4 * tid + 2], x3 = hb[4 * tid + 3];
+      const int t4 = x0 + x1 + x2 + x3;
+      const int e = wave_scan_i32(t4) - t4;
+      hb[4 * tid] = e; hb[4 * tid + 1] = e + x0; hb[4 * tid + 2] = e + x0 + x1; hb[4 * tid + 3] = e + x0 + x1 + x2;
+    }
+    __syncthreads();
+    for (int64_t t0 = 0; t0 < M; t0 += kRS) {  // stable multi-split, one tile of kRS entries
+      for (int k = tid; k < (kRS / 64) * 256; k += kRS) (&wc[0][0])[k] = 0;
+      const int64_t i = t0 + tid;
+      const bool v = i < M;
+      const uint32_t key = v ? sk[i] : 0u;
+      const int32_t val = v ? sv[i] : 0;
+      const uint32_t dg = (key >> sh) & 255u;
+      uint64_t m = ballot(v);
+#pragma unroll
+      for (int bit = 0; bit < 8; ++bit) {
+        const uint64_t bb = ballot(((dg >> bit) & 1u) != 0);
+        m &= ((dg >> bit) & 1u) ? bb : ~bb;
+      }
+      const int rank = __popcll(m & lt);
+      __syncthreads();
+      if (v && rank == 0) wc[w][dg] = __popcll(m);
+      __syncthreads();
+      if (tid < 256) {
+        int run = hb[tid];
+        for (int k = 0; k < kRS / 64; ++k) { const int c = wc[k][tid]; wc[k][tid] = run; run += c; }
+        hb[tid] = run;
+      }
+      __syncthreads();
+      if (v) { const int o = wc[w][dg] + rank; dk[o] = key; dv[o] = val; }
+      __syncthreads();
+    }
+  }
 }
 
 // rsl[g] = #mixed RIGHT events of this shard with gap < g; rpos[local read] =
 // its position in the shard's sorted list (so consumers need no search).  One
-// shard: right_start = rsl, roff = 0.  Several: per-gap counts for the exchange.
+// shard: right_start = rsl, roff = 0, and the RIGHT length of run t + g (the run
+// that this event closes) is filled here.  Several: per-gap counts for the
+// exchange (K_runs / K_runR).
 __global__ __launch_bounds__(256) void K_rstart(Dev d) {
   const int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t M = d.status[MPC_ST_MIXED];
   if (t <= d.G) {
-    const int32_t v = (int32_t)lower_bound_u32(d.keys_out, 0, d.N, (uint32_t)t);
+    const int32_t v = (int32_t)lower_bound_u32(d.keys_out, 0, M, (uint32_t)t);
     d.rsl[t] = v;
     if (d.n_shards == 1) { d.right_start[t] = v; d.roff[t] = 0; }
-    if (t < d.G) d.rcnt[t] = (int32_t)lower_bound_u32(d.keys_out, 0, d.N, (uint32_t)t + 1) - v;
+    if (t < d.G) d.rcnt[t] = (int32_t)lower_bound_u32(d.keys_out, 0, M, (uint32_t)t + 1) - v;
   }
-  if (t == 0) d.status[MPC_ST_MIXED] = (uint32_t)lower_bound_u32(d.keys_out, 0, d.N, (uint32_t)d.G);
-  if (t < d.N && d.keys_out[t] < (uint32_t)d.G) {
-    const int64_t lr = (int64_t)d.vals_out[t] - d.read_offset;
+  if (t < M) {
+    const uint32_t g = d.keys_out[t];
+    const int64_t rg = d.vals_out[t];
+    const int64_t lr = rg - d.read_offset;
     if (lr >= 0 && lr < d.N) d.rpos[lr] = (int32_t)t;
-  }
-}
-
-__global__ __launch_bounds__(256) void K_zero_runs(Dev d) {
-  const int64_t nruns = (int64_t)d.right_start[d.G] + d.G;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nruns; t += (int64_t)gridDim.x * blockDim.x) {
-    d.M[t] = 0;
+    if (d.n_shards == 1) d.runR[t + g] = d.rlen[rg];
   }
 }
 
@@ -750,9 +889,20 @@ __global__ __launch_bounds__(1024) void K_runs(Dev d) {
   }
 }
 
+// Several shards: RIGHT length of the run each of this shard's mixed RIGHT
+// events closes, in the global run index space (exchange: MAX over shards).
+__global__ __launch_bounds__(256) void K_runR(Dev d) {
+  const int64_t nml = d.rsl[d.G];
+  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nml; t += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t g = d.keys_out[t];
+    const int64_t run = (int64_t)d.right_start[g] + g + d.roff[g] + (t - d.rsl[g]);
+    d.runR[run] = d.rlen[d.vals_out[t]];
+  }
+}
+
 // Global run index of a LEFT event of (this shard's) global read rg at global
 // gap g: runs of gap g are [right_start[g] + g, right_start[g+1] + g + 1); run
-// k follows the k-th mixed RIGHT event of the gap, k = RIGHT events of lower
+// k precedes the k-th mixed RIGHT event of the gap, k = RIGHT events of lower
 // shards + this shard's RIGHT events of earlier reads.
 __device__ __forceinline__ int64_t run_left(const int32_t* rs, const int32_t* rsl, const int32_t* roff,
                                             const int32_t* vals_out, int64_t g, int64_t rg) {
@@ -763,14 +913,15 @@ __device__ __forceinline__ int64_t run_left(const int32_t* rs, const int32_t* rs
 }
 
 // ---------------------------------------------------------------------------
-// Bucketed event work units.  K_parse leaves, per parse workgroup, its events
-// counting-sorted into buckets of 16 gaps (insertion buckets [0, nbk), flank
-// buckets [nbk, 2 nbk)).  Entries of the host table `bc` are (sample, bucket,
-// chunk of <= 256 parse workgroups); K_units cuts every entry's events into
-// units of <= kUnit events (hot gaps -- every full-length read starts at gap 0
-// and ends at gap n -- become many units) and appends them to one list.
+// Bucketed event work units.  K_parse leaves, per parse workgroup, its
+// insertion events counting-sorted into buckets of 16 gaps.  Entries of the
+// host table `bc` are (sample, bucket, chunk of <= 256 parse workgroups);
+// K_units cuts every entry's events into units of <= kUnit events (hot
+// buckets become many units) and appends them to one list.
 // ---------------------------------------------------------------------------
-constexpr int kUnit = 1024;  // events per work unit
+constexpr int kUB = 1024;             // threads of the unit kernels (K_left, K_ins)
+constexpr int kEPT = 8;               // events per thread per unit (loads batched)
+constexpr int kUnit = kUB * kEPT;     // events per work unit
 
 struct UnitArgs {
   const int4* bc;  // {sample, bucket, pw0, pw1}
@@ -813,21 +964,26 @@ __device__ __forceinline__ UnitView load_unit(const int4* bc_tab, const int4* un
   const int4 un = units[u];
   const int4 bc = bc_tab[un.x];
   const int l = lane(), w = threadIdx.x >> 6;
-  const int pw = bc.z + (int)threadIdx.x;
-  int cnt = 0;
-  int64_t src = 0;
-  if (pw < bc.w) {
-    const int64_t slot = (int64_t)pw * nbs + bc.y;
-    cnt = bk_cnt[slot];
-    src = rbase[pw] + bk_off[slot];
+  if (threadIdx.x < 256) {  // <= 256 slices (parse workgroups) per table entry
+    const int pw = bc.z + (int)threadIdx.x;
+    int cnt = 0;
+    int64_t src = 0;
+    if (pw < bc.w) {
+      const int64_t slot = (int64_t)pw * nbs + bc.y;
+      cnt = bk_cnt[slot];
+      src = rbase[pw] + bk_off[slot];
+    }
+    const int inc = wave_scan_i32(cnt);
+    if (l == 63) s_wsum[w] = inc;
+    s_pre[threadIdx.x] = inc - cnt;
+    s_src[threadIdx.x] = src;
   }
-  const int inc = wave_scan_i32(cnt);
-  if (l == 63) s_wsum[w] = inc;
   __syncthreads();
-  int wpre = 0;
-  for (int k = 0; k < w; ++k) wpre += s_wsum[k];
-  s_pre[threadIdx.x] = wpre + inc - cnt;
-  s_src[threadIdx.x] = src;
+  if (threadIdx.x < 256) {
+    int wpre = 0;
+    for (int k = 0; k < w; ++k) wpre += s_wsum[k];
+    s_pre[threadIdx.x] += wpre;
+  }
   __syncthreads();
   return UnitView{bc.x, bc.y, un.y, un.z};
 }
@@ -840,17 +996,27 @@ __device__ __forceinline__ int64_t unit_event_src(const int32_t* s_pre, const in
   return s_src[lo] + (e - s_pre[lo]);
 }
 
+// per gap of a unit's 16-gap bucket: global run range and this shard's sorted-RIGHT range
+__device__ __forceinline__ void load_bucket_gaps(const int32_t* right_start, const int32_t* rsl, const int32_t* roff,
+                                                 int64_t g0, int ngap, int32_t* s_rs, int32_t* s_rsl, int32_t* s_roff) {
+  if ((int)threadIdx.x <= ngap) {
+    s_rs[threadIdx.x] = right_start[g0 + threadIdx.x];
+    s_rsl[threadIdx.x] = rsl[g0 + threadIdx.x];
+    s_roff[threadIdx.x] = roff[g0 + threadIdx.x];
+  }
+}
+
 // ---------------------------------------------------------------------------
 // K_left: LEFT events -> per-run max length M (the slot layout's input; the
-// bases themselves are tallied on rows by K_flank once the layout is known).
-// Persistent workgroups over the work units: a unit's events all lie in one
-// 16-gap bucket, so its (gap, run) maxima live in LDS (runs k < kKMax; rarer
-// runs go to HBM) and are flushed with atomics (several units may share a
-// bucket).  Insertions and upstream flanks are LEFT events; long insertions
-// (grid-stride tail) too.
+// bases themselves are tallied on rows once the layout is known).
+//  * insertions: persistent workgroups over the work units; a unit's events
+//    all lie in one 16-gap bucket, so its (gap, run) maxima live in LDS (runs
+//    k < kKMax; rarer runs go to HBM) and are flushed with atomics
+//  * long insertions and upstream flanks (one per read, LEFT at gap tstart,
+//    :303): grid-stride, wave-aggregated atomicMax (most reads share gap 0)
 // ---------------------------------------------------------------------------
 struct LeftArgs {
-  const int64_t* up_off; const int32_t* sample;
+  const int64_t* up_off; const int32_t* sample; const int32_t* tstart;
   const int32_t* n_of; const int32_t* gbase;
   const int4* bc; const int4* units; const uint32_t* status;
   const uint64_t* ins_sorted; const int32_t* bk_cnt; const int32_t* bk_off; const int64_t* rbase;
@@ -861,49 +1027,39 @@ struct LeftArgs {
   const Ovf* ovf; const uint32_t* ovf_cnt;
 };
 
-__global__ __launch_bounds__(256) void K_left(LeftArgs a) {
+__global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
+  __shared__ int64_t s_key;
+  __shared__ int32_t s_val;
   __shared__ uint32_t Ml[kBW][kKMax];
   __shared__ int32_t s_pre[256];
   __shared__ int64_t s_src[256];
   __shared__ int32_t s_wsum[4];
-  __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1];  // per gap of the bucket
+  __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1];  // per gap of the bucket (K_left)
   // (K_units raises DE_INTERNAL instead of overrunning the unit list)
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
     for (int k = threadIdx.x; k < kBW * kKMax; k += blockDim.x) (&Ml[0][0])[k] = 0;
-    {
-      const int4 bc = a.bc[a.units[u].x];
-      const int nn = a.n_of[bc.x];
-      const int nbk0 = (nn + 1 + kBW - 1) / kBW;
-      const int gg0 = (bc.y >= nbk0 ? bc.y - nbk0 : bc.y) * kBW;
-      const int gl = gg0 + kBW - 1 < nn ? gg0 + kBW - 1 : nn;
-      if ((int)threadIdx.x <= gl + 1 - gg0) {
-        const int64_t g = a.gbase[bc.x] + gg0 + threadIdx.x;
-        s_rs[threadIdx.x] = a.right_start[g];
-        s_rsl[threadIdx.x] = a.rsl[g];
-        s_roff[threadIdx.x] = a.roff[g];
-      }
-    }
     const UnitView uv = load_unit(a.bc, a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, s_pre, s_src, s_wsum);
     const int n = a.n_of[uv.smp];
     const int gb = a.gbase[uv.smp];
-    const int nbk = (n + 1 + kBW - 1) / kBW;
-    const int g0 = (uv.bucket >= nbk ? uv.bucket - nbk : uv.bucket) * kBW;
-    for (int e = uv.e0 + (int)threadIdx.x; e < uv.e0 + uv.cnt; e += blockDim.x) {
-      const uint64_t ev = a.ins_sorted[unit_event_src(s_pre, s_src, e)];
+    const int g0 = uv.bucket * kBW;
+    const int gl = g0 + kBW - 1 < n ? g0 + kBW - 1 : n;
+    load_bucket_gaps(a.right_start, a.rsl, a.roff, (int64_t)gb + g0, gl + 1 - g0, s_rs, s_rsl, s_roff);
+    __syncthreads();
+    uint64_t evs[kEPT];
+#pragma unroll
+    for (int q = 0; q < kEPT; ++q) {  // all loads first (latency), then the tallies
+      const int e = uv.e0 + (int)threadIdx.x + q * kUB;
+      evs[q] = e < uv.e0 + uv.cnt ? a.ins_sorted[unit_event_src(s_pre, s_src, e)] : ~0ull;
+    }
+#pragma unroll
+    for (int q = 0; q < kEPT; ++q) {
+      const uint64_t ev = evs[q];
       const int gap = (int)((ev >> 10) & kNullGap);
       if (gap > n || gap < g0 || gap >= g0 + kBW) continue;
       const int64_t g = (int64_t)gb + gap;
-      const int64_t rg = event_read(ev);
-      int L;
-      if (ev & kFlankBit) {
-        if (ev & kDownBit) continue;  // downstream flanks: RIGHT events (K_rsplit / K_seg_right)
-        const int64_t r = rg - a.read_offset;
-        const int64_t uln = a.up_off[r + 1] - a.up_off[r];
-        L = uln > 0x7fffffff ? 0x7fffffff : (int)uln;
-      } else {
-        L = (int)((ev >> 8) & 3u) + 1;
-      }
+      const int64_t rg = (int64_t)(ev >> 32);
+      const int L = (int)((ev >> 8) & 3u) + 1;
       const int p = gap - g0;
       const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
       const int64_t k = s_roff[p] + (lb > la ? lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la : 0);
@@ -918,13 +1074,35 @@ __global__ __launch_bounds__(256) void K_left(LeftArgs a) {
     }
     __syncthreads();
   }
-  // long insertions
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
+  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // long insertions
   const int64_t nov = *a.ovf_cnt < (uint32_t)a.ovf_cap ? *a.ovf_cnt : a.ovf_cap;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nov; t += nthreads) {
+  for (int64_t t = tid; t < nov; t += nthreads) {
     const Ovf o = a.ovf[t];
     const int64_t g = (int64_t)a.gbase[a.sample[o.read]] + o.gap;
     atomicMax(a.M + run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + o.read), o.len);
+  }
+  // upstream flanks (block-uniform trips: block_atomic_max synchronizes the block)
+  for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < a.N; r0 += nthreads) {
+    const int64_t r = r0 + threadIdx.x;
+    int64_t run = 0;
+    int32_t L = 0;
+    bool ok = false;
+    if (r < a.N) {
+      const int64_t ul = a.up_off[r + 1] - a.up_off[r];
+      const int s = a.sample[r];
+      const int ts = a.tstart[r];
+      if (ul > 0 && ts >= 0 && ts <= a.n_of[s]) {
+        const int64_t g = (int64_t)a.gbase[s] + ts;
+        run = a.right_start[g + 1] > a.right_start[g]
+                  ? run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + r)
+                  : (int64_t)a.right_start[g] + g;
+        L = ul > 0x7fffffff ? 0x7fffffff : (int32_t)ul;
+        ok = true;
+      }
+    }
+    block_atomic_max(a.M, run, L, ok, &s_key, &s_val);
   }
 }
 
@@ -934,93 +1112,122 @@ __global__ __launch_bounds__(256) void K_left(LeftArgs a) {
 // (RIGHT, left-justified).  State: lo = slots prepended, hi = slots appended.
 //   LEFT  len L : base bi -> absolute hi-1-bi ; lo = max(lo, L-hi)
 //   RIGHT len R : base bi -> absolute -lo+bi  ; hi = max(hi, R-lo)
-// Within a run of LEFT events hi is constant and within a run of RIGHT events
-// lo is constant, so only runs with a LEFT event (M>0) start a new segment.
+// Within a run of LEFT events hi is constant, so only the run's longest LEFT
+// string matters (M); run k is closed by the gap's k-th mixed RIGHT event
+// (length runR).  One thread per gap replays its runs; the per-block sums of
+// the row counts and of the depth difference array feed K_assemble's scans.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void K_seg_flags(Dev d) {
-  const int64_t nruns = (int64_t)d.right_start[d.G] + d.G;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nruns; t += (int64_t)gridDim.x * blockDim.x) {
-    d.hflag[t] = d.M[t] > 0 ? 1 : 0;
-    d.segR[t] = 0;
-  }
-}
+constexpr int kGB = 256;  // gaps per K_replay / K_assemble block
 
-// the first run of every gap is a segment head (separate launch: no race with K_seg_flags)
-__global__ __launch_bounds__(256) void K_seg_heads(Dev d) {
-  for (int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; g < d.G; g += (int64_t)gridDim.x * blockDim.x)
-    d.hflag[d.right_start[g] + g] = 1;
-}
-
-__global__ __launch_bounds__(256) void K_seg_right(Dev d) {
-  const int64_t nml = d.rsl[d.G];  // this shard's mixed RIGHT events
-  const int64_t nruns = (int64_t)d.right_start[d.G] + d.G;
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nml; t += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t g = d.keys_out[t];
-    const int64_t tg = (int64_t)d.right_start[g] + d.roff[g] + (t - d.rsl[g]);  // position in the global list
-    const int64_t seg = d.hscan[tg + g] - 1;  // segment of the run just before this RIGHT event
-    atomicMax(d.segR + seg, d.rlen[d.vals_out[t]]);
-  }
-  for (int64_t t = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; t < nruns; t += (int64_t)gridDim.x * blockDim.x)
-    if (d.hflag[t]) d.seg_run[d.hscan[t] - 1] = (int32_t)t;
-}
-
-__global__ __launch_bounds__(256) void K_replay(Dev d) {
-  const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-  if (g >= d.G) return;
-  const int64_t r0 = d.right_start[g] + g, r1 = d.right_start[g + 1] + g + 1;  // runs of gap g
-  const int64_t s0 = d.hscan[r0] - 1, s1 = d.hscan[r1 - 1];                   // segments [s0, s1)
-  int32_t lo = 0, hi = 0;
-  for (int64_t sidx = s0; sidx < s1; ++sidx) {
-    const int32_t m = d.M[d.seg_run[sidx]];
-    d.seg_hi[sidx] = hi;                       // hi seen by this run's LEFT events
-    if (m - hi > lo) lo = m - hi;
-    d.seg_lo[sidx] = lo;                       // lo seen by the RIGHT events of the segment
-    const int32_t R = d.segR[sidx];
-    if (R - lo > hi) hi = R - lo;
-  }
-  if (d.seg_run[s0] != r0) atomicOr(&d.status[MPC_ST_FLAGS], DE_INTERNAL);
-  // RIGHT-only gaps: their flanks were not sorted; slot bi = base bi
-  const int32_t mr = d.maxR[g];
-  if (mr - lo > hi) hi = mr - lo;
-  d.lo_f[g] = lo;
-  // rows of a gap = its slots + the odd position after it (if any)
-  int s = 0;
-  while (g >= d.gbase[s + 1]) ++s;
-  const int64_t p = g - d.gbase[s];
-  d.rowcnt[g] = lo + hi + (p < d.n_of[s] ? 1 : 0);
-}
-
-__global__ void K_rows_total(Dev d) {
-  const int64_t tot = (int64_t)d.row_base[d.G - 1] + d.rowcnt[d.G - 1];
-  d.status[MPC_ST_ROWS_NEEDED] = (uint32_t)tot;
-  if (tot > d.row_cap) atomicOr(&d.status[MPC_ST_FLAGS], DE_CAP);
-}
-
-// ---------------------------------------------------------------------------
-// Rows: one wave per gap zeroes the gap's slot rows (K_flank adds the
-// insertion and flank bases) and writes the odd-position row that follows it.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void K_assemble(Dev d) {
-  const int l = lane(), w = threadIdx.x >> 6;
-  if (d.status[MPC_ST_FLAGS] & DE_CAP) return;
-  const int64_t stride = (int64_t)gridDim.x * 4;
-  for (int64_t g = (int64_t)blockIdx.x * 4 + w; g < d.G; g += stride) {
-    int s = 0;
-    while (g >= d.gbase[s + 1]) ++s;
-    const int64_t p = g - d.gbase[s];
-    const int64_t n = d.n_of[s];
-    const int64_t rb = d.row_base[g];
-    const int64_t nslots = (int64_t)d.rowcnt[g] - (p < n ? 1 : 0);
-    for (int64_t k = l; k < nslots; k += 64) {
-      reinterpret_cast<uint4*>(d.rows)[rb + k] = make_uint4(0, 0, 0, 0);
-      d.meta[rb + k] = (k == 0) ? 2 : 0;
+__global__ __launch_bounds__(kGB) void K_replay(Dev d) {
+  __shared__ int32_t s_w[2][kGB / 64];
+  const int64_t g = (int64_t)blockIdx.x * kGB + threadIdx.x;
+  int32_t rc = 0, dv = 0;
+  if (g < d.G) {
+    const int64_t r0 = (int64_t)d.right_start[g] + g, r1 = (int64_t)d.right_start[g + 1] + g + 1;  // runs of gap g
+    int32_t lo = 0, hi = 0;
+    for (int64_t t = r0; t < r1; ++t) {
+      d.hiR[t] = hi;                          // hi seen by the run's LEFT events
+      const int32_t m = d.M[t];
+      if (m - hi > lo) lo = m - hi;
+      if (t + 1 < r1) {
+        d.loR[t] = lo;                        // lo seen by the RIGHT event closing the run
+        const int32_t R = d.runR[t];
+        if (R - lo > hi) hi = R - lo;
+      }
     }
-    if (p < n && l == 0 && d.shard != 0) {  // rows are summed over shards: odd rows come from shard 0
-      reinterpret_cast<uint4*>(d.rows)[rb + nslots] = make_uint4(0, 0, 0, 0);
-      d.meta[rb + nslots] = 3;
-    } else if (p < n && l == 0) {
+    // RIGHT-only gaps: their flanks were not sorted; slot bi = base bi
+    const int32_t mr = d.maxR[g];
+    if (mr - lo > hi) hi = mr - lo;
+    d.lo_f[g] = lo;
+    // rows of a gap = its slots + the odd position after it (if any)
+    int lo_s = 0, hi_s = d.S - 1;  // sample of gap g
+    while (lo_s < hi_s) {
+      const int mid = (lo_s + hi_s + 1) >> 1;
+      if (d.gbase[mid] <= g) lo_s = mid; else hi_s = mid - 1;
+    }
+    const int64_t p = g - d.gbase[lo_s];
+    rc = lo + hi + (p < d.n_of[lo_s] ? 1 : 0);
+    d.rowcnt[g] = rc;
+    dv = d.diff[g];
+  }
+  const int w = threadIdx.x >> 6;
+  rc = wave_sum(rc);
+  dv = wave_sum(dv);
+  if (lane() == 0) { s_w[0][w] = rc; s_w[1][w] = dv; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t a = 0, b = 0;
+    for (int k = 0; k < kGB / 64; ++k) { a += s_w[0][k]; b += s_w[1][k]; }
+    d.bsum[2 * blockIdx.x] = a;
+    d.bsum[2 * blockIdx.x + 1] = b;
+  }
+}
+
+// Block-level exclusive prefix of K_replay's block sums (pair = {rows, diff}).
+// Every block also gets the totals.  Returns {prefix_rows, prefix_diff, total_rows}.
+__device__ __forceinline__ int3 block_prefix_pairs(const int32_t* bsum, int64_t nb, int64_t b, int32_t* s_red) {
+  int64_t pr = 0, pd = 0, tr = 0;
+  for (int64_t k = threadIdx.x; k < nb; k += blockDim.x) {
+    const int32_t x = bsum[2 * k], y = bsum[2 * k + 1];
+    tr += x;
+    if (k < b) { pr += x; pd += y; }
+  }
+  const int w = threadIdx.x >> 6;
+  const int32_t a0 = wave_sum((int32_t)pr), a1 = wave_sum((int32_t)pd), a2 = wave_sum((int32_t)tr);
+  __syncthreads();
+  if (lane() == 0) { s_red[3 * w] = a0; s_red[3 * w + 1] = a1; s_red[3 * w + 2] = a2; }
+  __syncthreads();
+  int3 r = make_int3(0, 0, 0);
+  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { r.x += s_red[3 * k]; r.y += s_red[3 * k + 1]; r.z += s_red[3 * k + 2]; }
+  return r;
+}
+
+// ---------------------------------------------------------------------------
+// Rows: scans of the row counts (-> row_base) and of the depth difference
+// array (-> depth of odd position p), then the odd-position row of every gap
+// (depth - substitutions matched the reference base, :79) and the slot-0
+// marks.  Slot rows were zeroed by K_clear; the flank / insertion kernels add
+// to them.  Also the ROWS_NEEDED / capacity check (all blocks see the total).
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(kGB) void K_assemble(Dev d) {
+  __shared__ int32_t s_red[3 * (kGB / 64)];
+  __shared__ int32_t s_w[2][kGB / 64];
+  const int64_t nb = (d.G + kGB - 1) / kGB;
+  const int3 pre = block_prefix_pairs(d.bsum, nb, blockIdx.x, s_red);
+  const int64_t tot = pre.z;
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
+    d.status[MPC_ST_ROWS_NEEDED] = (uint32_t)tot;
+    if (tot > d.row_cap) atomicOr(&d.status[MPC_ST_FLAGS], DE_CAP);
+  }
+  const int64_t g = (int64_t)blockIdx.x * kGB + threadIdx.x;
+  const int32_t rc = g < d.G ? d.rowcnt[g] : 0;
+  const int32_t dv = g < d.G ? d.diff[g] : 0;
+  const int w = threadIdx.x >> 6;
+  const int ir = wave_scan_i32(rc), id = wave_scan_i32(dv);
+  if (lane() == 63) { s_w[0][w] = ir; s_w[1][w] = id; }
+  __syncthreads();
+  int32_t wr = 0, wd = 0;
+  for (int k = 0; k < w; ++k) { wr += s_w[0][k]; wd += s_w[1][k]; }
+  if (g >= d.G) return;
+  const int64_t rb = (int64_t)pre.x + wr + ir - rc;  // exclusive
+  const int64_t dep = (int64_t)pre.y + wd + id;      // inclusive
+  d.row_base[g] = (int32_t)rb;
+  if (tot > d.row_cap) return;
+  int lo_s = 0, hi_s = d.S - 1;
+  while (lo_s < hi_s) {
+    const int mid = (lo_s + hi_s + 1) >> 1;
+    if (d.gbase[mid] <= g) lo_s = mid; else hi_s = mid - 1;
+  }
+  const int s = lo_s;
+  const int64_t p = g - d.gbase[s];
+  const int64_t n = d.n_of[s];
+  const int64_t nslots = (int64_t)rc - (p < n ? 1 : 0);
+  if (nslots > 0) d.meta[rb] = 2;  // first slot of the gap
+  if (p < n) {
+    uint4 out = make_uint4(0, 0, 0, 0);
+    if (d.shard == 0) {  // rows are summed over shards: odd rows come from shard 0
       // odd position p: depth = reads covering p with a match or substitution
-      const int64_t dep = d.depth[g];
       const uint32_t* sb = d.sub + g * 4;
       const uint32_t s0 = sb[0], s1 = sb[1], s2 = sb[2], s3 = sb[3];
       const int64_t match = dep - (int64_t)s0 - s1 - s2 - s3;
@@ -1028,191 +1235,92 @@ __global__ __launch_bounds__(256) void K_assemble(Dev d) {
       uint32_t fl = 0;
       if (match < 0) fl |= DE_INTERNAL;
       else if (match > 0) {
-        const int rc = base_code_exact(d.ref[d.ref_off[s] + p]);
-        if (rc < 0) fl |= DE_KEY;  // refarr base not in the dict (:61)
-        else c[rc] += (uint32_t)match;
+        const int rcode = base_code_exact(d.ref[d.ref_off[s] + p]);
+        if (rcode < 0) fl |= DE_KEY;  // refarr base not in the dict (:61)
+        else c[rcode] += (uint32_t)match;
       }
       if (fl) atomicOr(&d.status[MPC_ST_FLAGS], fl);
-      reinterpret_cast<uint4*>(d.rows)[rb + nslots] = make_uint4(c[0], c[1], c[2], c[3]);
-      d.meta[rb + nslots] = 3;  // odd row, first (only) slot of its position
+      out = make_uint4(c[0], c[1], c[2], c[3]);
     }
+    reinterpret_cast<uint4*>(d.rows)[rb + nslots] = out;
+    d.meta[rb + nslots] = 3;  // odd row, first (only) slot of its position
   }
 }
 
 // ---------------------------------------------------------------------------
-// Slot tallies of the even positions (:37-72 applied to insertions and flank
-// strings).  Every inserted / flank base lands in the slot block of its anchor
-// gap, so a work unit (events of one 16-gap bucket) tallies the bucket's row
-// range in a dense LDS histogram -- bases processed flat across events, 4 per
-// lane -- then flushes with global atomics (hot buckets are split over several
-// units).  A grid-stride tail adds the long insertions.
+// Slot tallies of the even positions (:37-72 applied to insertion strings).
+// Every inserted base lands in the slot block of its anchor gap, so a work
+// unit (insertion events of one 16-gap bucket) tallies the bucket's row range
+// in a dense LDS histogram, then flushes with global atomics (hot buckets are
+// split over several units).  A grid-stride tail adds the long insertions.
 // ---------------------------------------------------------------------------
 constexpr int kFlankRows = 2048;  // dense LDS rows per unit (else HBM atomics)
 
-struct FlankArgs {
+struct InsArgs {
   uint32_t* status; const int32_t* sample; const int32_t* n_of; const int32_t* gbase;
   const int4* bc; const int4* units;
   const uint64_t* ins_sorted; const int32_t* bk_cnt; const int32_t* bk_off; const int64_t* rbase;
   int64_t N, read_offset, ovf_cap;
   int32_t nbs;
-  const int64_t* up_off; const uint8_t* up; const int64_t* down_off; const uint8_t* down;
   const int32_t* right_start; const int32_t* rsl; const int32_t* roff; const int32_t* vals_out;
-  const int32_t* row_base; const int32_t* rowcnt;
-  const int32_t* lo_f; const int32_t* seg_hi; const int32_t* seg_lo; const int32_t* hscan; const int32_t* rpos;
+  const int32_t* row_base; const int32_t* rowcnt; const int32_t* lo_f; const int32_t* hiR;
   uint32_t* rows; const Ovf* ovf; const uint32_t* ovf_cnt; const uint8_t* cs;
 };
 
-__global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
+__global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
   __shared__ uint32_t cnt[kFlankRows * 4];
   __shared__ int32_t s_pre[256];
   __shared__ int64_t s_src[256];
   __shared__ int32_t s_wsum[4];
-  __shared__ int64_t e_off[256], e_anc[256];
-  __shared__ int32_t e_pre[256], e_len[256];
-  __shared__ int32_t e_read[256];
-  __shared__ uint8_t e_down[256];
-  // per gap of the bucket: sorted-RIGHT range, row base, lo, hi of run 0
-  __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1], s_rowb[kBW], s_lof[kBW], s_hi0[kBW];
+  __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1], s_anc[kBW];
   const int l = lane();
   const int w = uniform_i32((int)(threadIdx.x >> 6));
   const int tid = threadIdx.x;
   if (a.status[MPC_ST_FLAGS] & DE_CAP) return;
-  uint32_t lerr = 0;
-  int64_t lread = -1;
   // (K_units raises DE_INTERNAL instead of overrunning the unit list)
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
-    {
-      const int4 bc = a.bc[a.units[u].x];
-      const int nn = a.n_of[bc.x];
-      const int nbk0 = (nn + 1 + kBW - 1) / kBW;
-      const int gg0 = (bc.y >= nbk0 ? bc.y - nbk0 : bc.y) * kBW;
-      const int gl = gg0 + kBW - 1 < nn ? gg0 + kBW - 1 : nn;
-      const int64_t gbb = a.gbase[bc.x];
-      if (tid <= gl + 1 - gg0) {
-        s_rs[tid] = a.right_start[gbb + gg0 + tid];
-        s_rsl[tid] = a.rsl[gbb + gg0 + tid];
-        s_roff[tid] = a.roff[gbb + gg0 + tid];
-      }
-      if (tid <= gl - gg0) {
-        const int64_t g = gbb + gg0 + tid;
-        s_rowb[tid] = a.row_base[g];
-        s_lof[tid] = a.lo_f[g];
-        s_hi0[tid] = a.seg_hi[a.hscan[a.right_start[g] + g] - 1];
-      }
-    }
     const UnitView uv = load_unit(a.bc, a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, s_pre, s_src, s_wsum);
     const int n = a.n_of[uv.smp];
     const int64_t gb = a.gbase[uv.smp];
-    const int nbk = (n + 1 + kBW - 1) / kBW;
-    const int g0 = (uv.bucket >= nbk ? uv.bucket - nbk : uv.bucket) * kBW;
+    const int g0 = uv.bucket * kBW;
     const int gl = (g0 + kBW - 1 < n ? g0 + kBW - 1 : n);  // last gap of the bucket
-    const int64_t R0 = s_rowb[0];
-    const int64_t R1 = (int64_t)s_rowb[gl - g0] + a.rowcnt[gb + gl];
+    load_bucket_gaps(a.right_start, a.rsl, a.roff, gb + g0, gl + 1 - g0, s_rs, s_rsl, s_roff);
+    if (tid <= gl - g0) s_anc[tid] = a.row_base[gb + g0 + tid] + a.lo_f[gb + g0 + tid] - 1;  // + hi of the run
+    const int64_t R0 = a.row_base[gb + g0];
+    const int64_t R1 = (int64_t)a.row_base[gb + gl] + a.rowcnt[gb + gl];
     const bool dense = R1 - R0 <= kFlankRows;
     if (dense)
       for (int k = tid; k < (int)(R1 - R0) * 4; k += blockDim.x) cnt[k] = 0;
     __syncthreads();
-    for (int e0 = uv.e0; e0 < uv.e0 + uv.cnt; e0 += 256) {
-      // one event per thread: anchor row and flank byte range
-      const int e = e0 + tid;
-      int len = 0;
-      int64_t off = 0, anc = 0;
-      bool down = false;
-      int64_t r = 0;
-      bool ins = false;
-      if (e < uv.e0 + uv.cnt) {
-        const uint64_t ev = a.ins_sorted[unit_event_src(s_pre, s_src, e)];
-        const int gap = (int)((ev >> 10) & kNullGap);
-        const int p = gap - g0;
-        const int64_t rg = event_read(ev);
-        r = rg - a.read_offset;
-        ins = !(ev & kFlankBit);
-        down = (ev & kDownBit) != 0;
-        const int64_t g = gb + gap;
-        const int32_t ra = s_rs[p], rb = s_rs[p + 1];
-        int64_t L;
-        if (!down) {  // LEFT at gap tstart: base bi (from the 3' end) -> row lo + hi_run - 1 - bi
-          int32_t hi = s_hi0[p];
-          if (rb > ra) {  // mixed gap: run k = RIGHT events of earlier reads (all shards)
-            const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
-            const int64_t k = s_roff[p] + (lb > la ? lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la : 0);
-            hi = a.seg_hi[a.hscan[ra + g + k] - 1];
-          }
-          anc = (int64_t)s_rowb[p] + s_lof[p] + hi - 1;
-          if (ins) {  // inline insertion: 2-bit codes in the event word, string order; tallied here
-            const int Li = (int)((ev >> 8) & 3u) + 1;
-            for (int k = 0; k < Li; ++k) {
-              const int code = (int)((ev >> (2 * k)) & 3u);
-              const int64_t row = anc - (Li - 1 - k);
-              if (dense && row >= R0 && row < R1) atomicAdd(cnt + (row - R0) * 4 + code, 1u);
-              else atomicAdd(a.rows + row * 4 + code, 1u);
-            }
-            L = 0;
-          } else {
-            off = a.up_off[r];
-            L = a.up_off[r + 1] - off;
-          }
-        } else {      // RIGHT at gap i_end: base bi -> row lo - lo_at + bi
-          int64_t lo_at = 0;
-          bool ok = true;
-          if (rb > ra) {  // mixed gap: this read's RIGHT event in the (global) sorted list
-            const int64_t t = a.rpos[r];
-            const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
-            ok = t >= la && t < lb;
-            if (ok) lo_at = a.seg_lo[a.hscan[ra + s_roff[p] + (t - la) + g] - 1];
-            else lerr |= DE_INTERNAL;
-          }
-          anc = (int64_t)s_rowb[p] + s_lof[p] - lo_at;
-          off = a.down_off[r];
-          L = ok ? a.down_off[r + 1] - off : 0;
-        }
-        len = L > (1 << 30) ? (1 << 30) : (int)L;
-      }
-      const int nch = (len + 3) >> 2;  // 4-byte chunks of this flank
-      {  // block scan of chunk counts
-        const int inc = wave_scan_i32(nch);
-        __syncthreads();
-        if (l == 63) s_wsum[w] = inc;
-        __syncthreads();
-        int wpre = 0;
-        for (int k = 0; k < w; ++k) wpre += s_wsum[k];
-        e_pre[tid] = wpre + inc - nch;
-        e_len[tid] = len;
-        e_off[tid] = off;
-        e_anc[tid] = anc;
-        e_read[tid] = (int32_t)r;
-        e_down[tid] = down ? 1 : 0;
-      }
-      const int nchunks = s_wsum[0] + s_wsum[1] + s_wsum[2] + s_wsum[3];
-      __syncthreads();
-      for (int x = tid; x < nchunks; x += blockDim.x) {
-        int lo = 0, hi = 255;  // last event j with e_pre[j] <= x
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (e_pre[mid] <= x) lo = mid; else hi = mid - 1;
-        }
-        const int b0 = 4 * (x - e_pre[lo]);
-        const int L = e_len[lo];
-        const bool dn = e_down[lo] != 0;
-        uint32_t c4[4];
-        const uint8_t* src8 = (dn ? a.down : a.up) + e_off[lo];
+    uint64_t evs[kEPT];
 #pragma unroll
-        for (int k = 0; k < 4; ++k) c4[k] = b0 + k < L ? src8[b0 + k] : 0u;
-        const int64_t anc = e_anc[lo];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int bi = b0 + k;
-          if (bi >= L) break;
-          const int code = base_code_exact(c4[k]);
-          if (code < 0) { lerr |= DE_KEY; lread = e_read[lo]; continue; }  // flank base not in the dict (:61, :71)
-          const int64_t row = dn ? anc + bi : anc - (L - 1 - bi);
-          if (dense && row >= R0 && row < R1) atomicAdd(cnt + (row - R0) * 4 + code, 1u);
-          else atomicAdd(a.rows + row * 4 + code, 1u);
-        }
-      }
-      __syncthreads();
+    for (int q = 0; q < kEPT; ++q) {  // all loads first (latency), then the tallies
+      const int e = uv.e0 + tid + q * kUB;
+      evs[q] = e < uv.e0 + uv.cnt ? a.ins_sorted[unit_event_src(s_pre, s_src, e)] : ~0ull;
     }
+#pragma unroll
+    for (int q = 0; q < kEPT; ++q) {
+      const uint64_t ev = evs[q];
+      const int gap = (int)((ev >> 10) & kNullGap);
+      if (gap > n || gap < g0 || gap > gl) continue;
+      const int p = gap - g0;
+      int64_t anc = s_anc[p];  // LEFT: base bi (from the 3' end) -> row lo + hi_run - 1 - bi
+      if (s_rs[p + 1] > s_rs[p]) {  // mixed gap: run k = RIGHT events of earlier reads (all shards)
+        const int64_t rg = (int64_t)(ev >> 32);
+        const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
+        const int64_t k = s_roff[p] + (lb > la ? lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la : 0);
+        anc += a.hiR[s_rs[p] + gb + gap + k];
+      }
+      const int Li = (int)((ev >> 8) & 3u) + 1;  // inline insertion: 2-bit codes in string order
+      for (int k = 0; k < Li; ++k) {
+        const int code = (int)((ev >> (2 * k)) & 3u);
+        const int64_t row = anc - (Li - 1 - k);
+        if (dense && row >= R0 && row < R1) atomicAdd(cnt + (row - R0) * 4 + code, 1u);
+        else atomicAdd(a.rows + row * 4 + code, 1u);
+      }
+    }
+    __syncthreads();
     if (dense)
       for (int k = tid; k < (int)(R1 - R0) * 4; k += blockDim.x) {
         const uint32_t v = cnt[k];
@@ -1222,19 +1330,189 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
   }
   // long insertions (grid-stride, LEFT like the short ones)
   const int64_t nov = *a.ovf_cnt < (uint32_t)a.ovf_cap ? *a.ovf_cnt : a.ovf_cap;
-  for (int64_t t = (int64_t)blockIdx.x * 4 + w; t < nov; t += (int64_t)gridDim.x * 4) {
+  for (int64_t t = (int64_t)blockIdx.x * (kUB / 64) + w; t < nov; t += (int64_t)gridDim.x * (kUB / 64)) {
     const Ovf o = a.ovf[t];
     const int64_t g = a.gbase[a.sample[o.read]] + o.gap;
     const int64_t run = run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + o.read);
-    const int64_t rb = (int64_t)a.row_base[g] + a.lo_f[g] + a.seg_hi[a.hscan[run] - 1] - 1;
+    const int64_t rb = (int64_t)a.row_base[g] + a.lo_f[g] + a.hiR[run] - 1;
     for (int64_t bi = l; bi < o.len; bi += 64) {
       const int c = code_upper(a.cs[o.off + o.len - 1 - bi]);
       atomicAdd(a.rows + (rb - bi) * 4 + (c < 0 ? 0 : c), 1u);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Flank tallies, read-parallel.  Every read's upstream flank (LEFT at gap
+// tstart, :303 -> :37-62) and downstream flank (RIGHT at gap i_end, :323 ->
+// :64-72) map LINEARLY onto rows once the layout is known: byte j of the flank
+// goes to row rowstart + j, with
+//   upstream   rowstart = row_base + lo_f + hi_run - L
+//   downstream rowstart = row_base + lo_f - lo_at
+// (hi_run / lo_at = 0 unless the gap is mixed).  A block takes kFR
+// consecutive reads: their flank bytes are contiguous, so the block streams
+// them with coalesced dword loads, flat over bytes.  Rows of the first read's
+// gap (for full-length reads: gap 0 upstream, gap n downstream -- the hot
+// gaps) are tallied in LDS windows, everything else with global atomics.
+// ---------------------------------------------------------------------------
+constexpr int kFR = 256;        // reads per block (one per thread)
+constexpr int kWinRows = 256;   // LDS window rows per flank side
+
+struct FlankArgs {
+  uint32_t* status; const int32_t* sample; const int32_t* n_of; const int32_t* gbase;
+  const int32_t* tstart; const int32_t* i_end;
+  const int64_t* up_off; const uint8_t* up; const int64_t* down_off; const uint8_t* down;
+  const int32_t* right_start; const int32_t* rsl; const int32_t* roff; const int32_t* vals_out; const int32_t* rpos;
+  const int32_t* row_base; const int32_t* lo_f; const int32_t* hiR; const int32_t* loR;
+  uint32_t* rows;
+  int64_t N, read_offset;
+};
+
+// dict code of an exact-case base (flanks are upper-cased at ingest, :270):
+// h = (c >> 1) & 3 is a perfect hash A0 C1 T2 G3 on "ACTG", bit-swapped to A0 T1 C2 G3
+__device__ __forceinline__ int code_exact(uint32_t c) {
+  const uint32_t h = (c >> 1) & 3u;
+  const uint32_t expect = (0x47544341u >> (8 * h)) & 0xffu;
+  const int code = (int)(((h & 1u) << 1) | (h >> 1));
+  return c == expect ? code : -1;
+}
+
+constexpr int kStageB = 8192;  // flank bytes staged in LDS per side (the rest is read from HBM directly)
+
+__global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
+  __shared__ uint32_t win[2][kWinRows * 4];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[2][kStageB + 16];
+  __shared__ int32_t s_gap[2][kFR];
+  __shared__ int64_t s_w0[2];
+  if (a.status[MPC_ST_FLAGS] & (DE_CAP | DE_INTERNAL)) return;
+  const int tid = threadIdx.x;
+  const int64_t r0 = (int64_t)blockIdx.x * kFR;
+  const int64_t r1 = r0 + kFR < a.N ? r0 + kFR : a.N;
+  const int nr = (int)(r1 - r0);
+  const int64_t tot = a.status[MPC_ST_ROWS_NEEDED];
+  const int64_t r = r0 + tid;
+  const bool live = tid < nr;
+  // level 1: per-read records and the block's byte ranges (independent loads)
+  int s = 0, ts = 0, ie = 0;
+  int64_t off[2] = {0, 0}, end[2] = {0, 0};
+  if (live) {
+    s = a.sample[r]; ts = a.tstart[r]; ie = a.i_end[r];
+    off[0] = a.up_off[r]; end[0] = a.up_off[r + 1];
+    off[1] = a.down_off[r]; end[1] = a.down_off[r + 1];
+  }
+  const int64_t B0[2] = {a.up_off[r0], a.down_off[r0]};
+  const int64_t B1[2] = {a.up_off[r1], a.down_off[r1]};
+  // level 2: stage the block's flank bytes (16 B per lane, coalesced) while the layout loads fly
+  int64_t A0[2];
+#pragma unroll
+  for (int side = 0; side < 2; ++side) {
+    const uint8_t* src = side ? a.down : a.up;
+    A0[side] = B0[side] & ~(int64_t)15;
+    const int64_t nb = B1[side] - A0[side];
+    const int64_t nst = nb < kStageB ? nb : kStageB;
+#ifdef MPC_EXP_NOSTAGE_FLANK
+    for (int64_t x = 16 * tid; x < 0; x += 16 * blockDim.x)
+#else
+    for (int64_t x = 16 * tid; x < nst; x += 16 * blockDim.x)
+#endif
+      *reinterpret_cast<uint4*>(&stage[side][x]) = *reinterpret_cast<const uint4*>(src + A0[side] + x);
+  }
+  for (int k = tid; k < 2 * kWinRows * 4; k += blockDim.x) (&win[0][0])[k] = 0;
+  int64_t rs[2] = {-1, -1};
+  int32_t gap[2] = {-1, -1};
+  if (live) {
+    const int n = a.n_of[s];
+    const int64_t gb = a.gbase[s];
+    const int64_t ul = end[0] - off[0];
+    if (ul > 0 && ts >= 0 && ts <= n) {  // LEFT at gap tstart: byte j -> row_base + lo_f + hi_run - L + j
+      const int64_t g = gb + ts;
+      int64_t hi = 0;
+      if (a.right_start[g + 1] > a.right_start[g])
+        hi = a.hiR[run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + r)];
+      rs[0] = (int64_t)a.row_base[g] + a.lo_f[g] + hi - ul;
+      gap[0] = (int32_t)g;
+    }
+    const int64_t dl = end[1] - off[1];
+    if (dl > 0 && ie >= 0 && ie <= n) {  // RIGHT at gap i_end: byte j -> row_base + lo_f - lo_at + j
+      const int64_t g = gb + ie;
+      int64_t lo_at = 0;
+      if (a.right_start[g + 1] > a.right_start[g]) {
+        const int64_t t = a.rpos[r];
+        lo_at = a.loR[(int64_t)a.right_start[g] + g + a.roff[g] + (t - a.rsl[g])];
+      }
+      rs[1] = (int64_t)a.row_base[g] + a.lo_f[g] - lo_at;
+      gap[1] = (int32_t)g;
+    }
+  }
+  s_gap[0][tid] = gap[0];
+  s_gap[1][tid] = gap[1];
+  __syncthreads();
+  if (tid < 2) {  // LDS window: rows of the gap most of the block's reads use (vote of 3 reads)
+    const int32_t x = s_gap[tid][0], y = s_gap[tid][nr / 2], z = s_gap[tid][nr - 1];
+    const int32_t gw = (x == y || x == z) ? x : y;
+    s_w0[tid] = gw >= 0 ? (int64_t)a.row_base[gw] : (int64_t)INT32_MIN;
+  }
+  __syncthreads();
+  uint32_t lerr = 0;
+#pragma unroll 1
+#ifdef MPC_EXP_NOLOOP_FLANK
+  for (int side = 0; side < 0; ++side) {
+#else
+  for (int side = 0; side < 2; ++side) {
+#endif
+    const int64_t w0 = s_w0[side];
+    uint32_t* wn = win[side];
+    const int64_t o = off[side];
+    const int64_t rsg = rs[side];
+    const int64_t Lg = rsg >= 0 ? end[side] - o : 0;
+    if (Lg > 0 && rsg + Lg > tot) lerr |= DE_INTERNAL;
+    const int L = (Lg > 0 && rsg + Lg <= tot) ? (int)(Lg > (1 << 30) ? (1 << 30) : Lg) : 0;
+    // staged bytes come from LDS, the rest (a very long block range) from HBM; generic pointer
+    const int64_t rel = o - A0[side];
+#ifdef MPC_EXP_NOSTAGE_FLANK
+    const bool staged = false;
+#else
+    const bool staged = rel + L <= kStageB;
+#endif
+    const uint8_t* src = staged ? &stage[side][0] + rel : (side ? a.down : a.up) + o;
+    const uint8_t* base = reinterpret_cast<const uint8_t*>((uintptr_t)src & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
+    const int64_t rw = rsg - w0;  // window row of byte 0
+    // chunks of 4 bytes in a per-lane rotated order: lanes of a wave hit different
+    // rows (every downstream flank starts at the same row, LDS atomics would collide)
+    const int nch = (L + 3) >> 2;
+    int c = nch > 0 ? (int)(lane() % nch) : 0;
+    for (int it = 0; it < nch; ++it, c = (c + 1 == nch) ? 0 : c + 1) {
+      const int j = 4 * c;
+      const uint32_t v = __builtin_amdgcn_alignbyte(*reinterpret_cast<const uint32_t*>(base + j + 4),
+                                                    *reinterpret_cast<const uint32_t*>(base + j), sh);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int jj = j + k;
+        if (jj >= L) break;
+        const int code = code_exact((v >> (8 * k)) & 0xffu);
+        if (code < 0) { lerr |= DE_KEY; continue; }  // flank base not in the dict (:61, :71)
+        const int64_t wr = rw + jj;
+        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 4 + code, 1u);
+        else atomicAdd(a.rows + (rsg + jj) * 4 + code, 1u);
+      }
+    }
+  }
+  __syncthreads();
+#ifdef MPC_EXP_NOFLUSH_FLANK
+  for (int side = 0; side < 0; ++side) {
+#else
+  for (int side = 0; side < 2; ++side) {
+#endif
+    const int64_t w0 = s_w0[side];
+    for (int k = tid; k < kWinRows * 4; k += blockDim.x) {
+      const uint32_t v = win[side][k];
+      if (v) atomicAdd(a.rows + w0 * 4 + k, v);
+    }
+  }
   if (lerr) {
     atomicOr(&a.status[MPC_ST_FLAGS], lerr);
-    if (lread >= 0) atomicMin(&a.status[MPC_ST_FIRST_READ], (uint32_t)lread);
+    if (lerr & DE_KEY) atomicMin(&a.status[MPC_ST_FIRST_READ], (uint32_t)r);
   }
 }
 
@@ -1242,12 +1520,17 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
 // Consensus (Steps 5-6, :332-439)
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ int sample_of_row(const Dev& d, int64_t row) {
-  int s = 0;
-  while (s + 1 < d.S && row >= d.row_base[d.gbase[s + 1]]) ++s;
-  return s;
+  int lo = 0, hi = d.S - 1;  // last sample whose first row <= row
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (d.row_base[d.gbase[mid]] <= row) lo = mid; else hi = mid - 1;
+  }
+  return lo;
 }
 
 __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
+  __shared__ int64_t s_key;
+  __shared__ int32_t s_val;
   const bool cap = (d.status[MPC_ST_FLAGS] & DE_CAP) != 0;
   const int64_t need = cap ? 0 : (int64_t)d.status[MPC_ST_ROWS_NEEDED];
   for (int64_t row0 = (int64_t)blockIdx.x * blockDim.x; row0 < R; row0 += (int64_t)gridDim.x * blockDim.x) {
@@ -1285,48 +1568,82 @@ __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
       }
     }
     if (row < R) reinterpret_cast<uint4*>(d.res)[row] = out;
-    // max depth: one atomic per wave when the wave's slot-0 rows share a sample
-    const uint64_t act = ballot(smp >= 0);
-    if (act) {
-      const int lead = __ffsll((unsigned long long)act) - 1;
-      const int s0 = __shfl(smp, lead, 64);
-      const bool same = (smp < 0) || smp == s0;
-      if (ballot(!same)) {
-        if (smp >= 0) atomicMax(d.maxdepth + smp, slot0);
-      } else {
-        const uint32_t mx = (uint32_t)wave_max((int)slot0);
-        if (lane() == 0) atomicMax(d.maxdepth + s0, mx);
-      }
-    }
+    // max depth: block-aggregated (same-address atomics serialize)
+    block_atomic_max(reinterpret_cast<int32_t*>(d.maxdepth), smp, (int32_t)slot0, smp >= 0, &s_key, &s_val);
   }
+}
+
+// keep[row] = emitted (:428) and per-block counts (kKB rows per block)
+constexpr int kKB = 1024;
+__device__ __forceinline__ bool keep_row(const Dev& d, int64_t row, uint4 v) {
+  if (!(v.x >> 24)) return false;
+  const int s = sample_of_row(d, row);
+  const double thr = (double)d.maxdepth[s] * d.mdf;  // :338
+  return (double)v.y > thr;                           // :428
 }
 
 __global__ __launch_bounds__(256) void K_keep(Dev d, int64_t R) {
-  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < R; row += (int64_t)gridDim.x * blockDim.x) {
-    const uint4 v = reinterpret_cast<const uint4*>(d.res)[row];
-    int k = 0;
-    if (v.x >> 24) {
-      const int s = sample_of_row(d, row);
-      const double thr = (double)d.maxdepth[s] * d.mdf;   // :338
-      k = (double)v.y > thr ? 1 : 0;                        // :428
-    }
-    d.keep[row] = k;
+  __shared__ int32_t s_w[4];
+  const int64_t base = (int64_t)blockIdx.x * kKB + 4 * threadIdx.x;
+  int c = 0;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t row = base + k;
+    if (row < R && keep_row(d, row, reinterpret_cast<const uint4*>(d.res)[row])) { ++c; bits |= 1u << k; }
   }
+  d.keep[(int64_t)blockIdx.x * 256 + threadIdx.x] = (int32_t)bits;
+  c = wave_sum(c);
+  if (lane() == 0) s_w[threadIdx.x >> 6] = c;
+  __syncthreads();
+  if (threadIdx.x == 0) d.ksum[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
 __global__ __launch_bounds__(256) void K_emit(Dev d, int64_t R) {
-  for (int64_t row = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; row < R; row += (int64_t)gridDim.x * blockDim.x) {
-    if (d.keep[row]) {
-      const uint4 v = reinterpret_cast<const uint4*>(d.res)[row];
-      reinterpret_cast<uint4*>(d.calls)[d.keep_scan[row]] = make_uint4(v.x & 0xffffffu, v.y, v.z, v.w);
+  __shared__ int32_t s_red[4], s_w[4];
+  const int64_t nb = (R + kKB - 1) / kKB;
+  int64_t pre = 0, all = 0;
+  for (int64_t k = threadIdx.x; k < nb; k += blockDim.x) {
+    const int32_t x = d.ksum[k];
+    all += x;
+    if (k < (int64_t)blockIdx.x) pre += x;
+  }
+  const int w = threadIdx.x >> 6;
+  {
+    const int32_t a0 = wave_sum((int32_t)pre), a1 = wave_sum((int32_t)all);
+    if (lane() == 0) { s_red[w] = a0; s_w[w] = a1; }
+    __syncthreads();
+    pre = s_red[0] + s_red[1] + s_red[2] + s_red[3];
+    all = s_w[0] + s_w[1] + s_w[2] + s_w[3];
+    __syncthreads();
+  }
+  const uint32_t bits = (uint32_t)d.keep[(int64_t)blockIdx.x * 256 + threadIdx.x];
+  const int c = __popc(bits);
+  const int inc = wave_scan_i32(c);
+  if (lane() == 63) s_red[w] = inc;
+  __syncthreads();
+  int wpre = 0;
+  for (int k = 0; k < w; ++k) wpre += s_red[k];
+  int64_t pos = pre + wpre + inc - c;
+  const int64_t base = (int64_t)blockIdx.x * kKB + 4 * threadIdx.x;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (bits & (1u << k)) {
+      const uint4 v = reinterpret_cast<const uint4*>(d.res)[base + k];
+      reinterpret_cast<uint4*>(d.calls)[pos++] = make_uint4(v.x & 0xffffffu, v.y, v.z, v.w);
     }
   }
-  if (blockIdx.x == 0) {
-    for (int s = threadIdx.x; s <= d.S; s += blockDim.x) {
-      const int64_t rb = s < d.S ? (int64_t)d.row_base[d.gbase[s]] : R;
-      d.ncalls[s] = rb < R ? d.keep_scan[rb] : (R > 0 ? d.keep_scan[R - 1] + d.keep[R - 1] : 0);
+  // ncalls[s] = calls before the first row of sample s; ncalls[S] = all
+  const int64_t b0 = (int64_t)blockIdx.x * kKB;
+  for (int s = 0; s < d.S; ++s) {
+    const int64_t rb = d.row_base[d.gbase[s]];
+    if (rb >= b0 && rb < b0 + kKB && (rb - b0) / 4 == threadIdx.x) {
+      int64_t q = pre + wpre + inc - c;
+      for (int k = 0; k < (int)((rb - b0) & 3); ++k) q += (bits >> k) & 1u;
+      d.ncalls[s] = (int32_t)q;
     }
   }
+  if (blockIdx.x == 0 && threadIdx.x == 0) d.ncalls[d.S] = (int32_t)all;
 }
 
 }  // namespace
@@ -1353,7 +1670,6 @@ struct mpc_plan {
   int end_bit = 0;
   size_t ws_bytes = 0;
   uint8_t* ws = nullptr;
-  size_t cub_tmp = 0;
   std::vector<int32_t> work_parse, work_bc;  // int4 records
   int n_parse_wg = 0, parse_lds = 0, nbmax = 1;
   int64_t n_bc = 0, units_cap = 0;
@@ -1361,9 +1677,9 @@ struct mpc_plan {
   bool fused = false;
   enum {
     B_STATUS, B_NOF, B_GBASE, B_IEND, B_INSRAW, B_INSSORT, B_BKCNT, B_BKOFF, B_RBASE, B_OVF, B_OVFCNT,
-    B_HASLEFT, B_MAXR, B_KIN, B_VIN, B_KOUT, B_VOUT, B_RLEN, B_RPOS, B_RSTART, B_RSLOC, B_ROFF, B_RCNT, B_RCNTALL, B_DIFF, B_SUB, B_M,
-    B_HFLAG, B_HSCAN, B_SEGR, B_SEGLO, B_SEGHI, B_SEGRUN, B_LOF, B_ROWCNT, B_ROWBASE, B_DEPTH, B_ROWS,
-    B_META, B_RES, B_KEEP, B_KEEPSCAN, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_CUB, B_COUNT
+    B_HASLEFT, B_MAXR, B_KIN, B_VIN, B_KOUT, B_VOUT, B_KTMP, B_VTMP, B_BCNT, B_BPRE, B_RLEN, B_RPOS, B_RSTART, B_RSLOC, B_ROFF, B_RCNT, B_RCNTALL,
+    B_DIFF, B_SUB, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
+    B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -1386,18 +1702,19 @@ Dev mpc_plan::dev() const {
   d.hasleft = at<uint32_t>(this, B_HASLEFT); d.maxR = at<int32_t>(this, B_MAXR);
   d.keys_in = at<uint32_t>(this, B_KIN); d.vals_in = at<int32_t>(this, B_VIN);
   d.keys_out = at<uint32_t>(this, B_KOUT); d.vals_out = at<int32_t>(this, B_VOUT);
+  d.keys_tmp = at<uint32_t>(this, B_KTMP); d.vals_tmp = at<int32_t>(this, B_VTMP);
+  d.bcnt = at<int32_t>(this, B_BCNT); d.bpre = at<int32_t>(this, B_BPRE);
   d.rlen = at<int32_t>(this, B_RLEN); d.rpos = at<int32_t>(this, B_RPOS); d.right_start = at<int32_t>(this, B_RSTART);
   d.rsl = at<int32_t>(this, B_RSLOC); d.roff = at<int32_t>(this, B_ROFF); d.rcnt = at<int32_t>(this, B_RCNT);
   d.rcnt_all = at<int32_t>(this, B_RCNTALL); d.shard = shard; d.n_shards = n_shards;
   d.diff = at<int32_t>(this, B_DIFF); d.sub = at<uint32_t>(this, B_SUB);
-  d.M = at<int32_t>(this, B_M);
-  d.hflag = at<int32_t>(this, B_HFLAG); d.hscan = at<int32_t>(this, B_HSCAN);
-  d.segR = at<int32_t>(this, B_SEGR); d.seg_lo = at<int32_t>(this, B_SEGLO); d.seg_hi = at<int32_t>(this, B_SEGHI);
-  d.seg_run = at<int32_t>(this, B_SEGRUN);
+  d.M = at<int32_t>(this, B_M); d.runR = at<int32_t>(this, B_RUNR);
+  d.hiR = at<int32_t>(this, B_HIR); d.loR = at<int32_t>(this, B_LOR);
   d.lo_f = at<int32_t>(this, B_LOF); d.rowcnt = at<int32_t>(this, B_ROWCNT); d.row_base = at<int32_t>(this, B_ROWBASE);
-  d.depth = at<int32_t>(this, B_DEPTH); d.rows = at<uint32_t>(this, B_ROWS); d.meta = at<uint8_t>(this, B_META);
+  d.bsum = at<int32_t>(this, B_BSUM);
+  d.rows = at<uint32_t>(this, B_ROWS); d.meta = at<uint8_t>(this, B_META);
   d.row_cap = row_cap;
-  d.res = at<uint32_t>(this, B_RES); d.keep = at<int32_t>(this, B_KEEP); d.keep_scan = at<int32_t>(this, B_KEEPSCAN);
+  d.res = at<uint32_t>(this, B_RES); d.keep = at<int32_t>(this, B_KEEP); d.ksum = at<int32_t>(this, B_KSUM);
   d.calls = at<uint32_t>(this, B_CALLS); d.ncalls = at<int32_t>(this, B_NCALLS); d.maxdepth = at<uint32_t>(this, B_MAXD);
   return d;
 }
@@ -1408,7 +1725,7 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.n_of = d.n_of; a.gbase = d.gbase;
   a.work = reinterpret_cast<const int4*>(p->ws + p->off[mpc_plan::B_WPARSE]);
   a.cs_base = d.cs_base; a.ovf_cap = d.ovf_cap; a.read_offset = d.read_offset; a.n_reads = d.N;
-  a.fused = p->fused ? 1 : 0; a.nbs = 2 * p->nbmax;
+  a.fused = p->fused ? 1 : 0; a.nbs = p->nbmax;
   a.i_end = d.i_end;
   a.ins_raw = at<uint64_t>(p, mpc_plan::B_INSRAW); a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
@@ -1427,12 +1744,12 @@ static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
 
 static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
   LeftArgs a;
-  a.up_off = d.up_off; a.sample = d.sample; a.n_of = d.n_of; a.gbase = d.gbase;
+  a.up_off = d.up_off; a.sample = d.sample; a.tstart = d.tstart; a.n_of = d.n_of; a.gbase = d.gbase;
   a.bc = at<const int4>(p, mpc_plan::B_WBC); a.units = at<const int4>(p, mpc_plan::B_UNITS); a.status = d.status;
   a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
   a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
-  a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = 2 * p->nbmax;
+  a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = p->nbmax;
   a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out; a.M = d.M;
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt;
   return a;
@@ -1442,33 +1759,44 @@ static UnitArgs unit_args(const mpc_plan* p, const Dev& d) {
   UnitArgs a;
   a.bc = at<const int4>(p, mpc_plan::B_WBC); a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT);
   a.units = at<int4>(p, mpc_plan::B_UNITS); a.status = d.status;
-  a.n_bc = p->n_bc; a.units_cap = p->units_cap; a.nbs = 2 * p->nbmax;
+  a.n_bc = p->n_bc; a.units_cap = p->units_cap; a.nbs = p->nbmax;
   return a;
 }
-static int64_t left_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 1024)); }
-static int64_t flank_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 768)); }
+static int64_t left_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 512)); }
+static int64_t ins_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 512)); }
+static int64_t flank_grid(const mpc_plan* p) { return std::max<int64_t>(1, (p->N + kFR - 1) / kFR); }
 
-static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
-  FlankArgs a;
+static InsArgs ins_args(const mpc_plan* p, const Dev& d) {
+  InsArgs a;
   a.status = d.status; a.sample = d.sample; a.n_of = d.n_of; a.gbase = d.gbase;
   a.bc = at<const int4>(p, mpc_plan::B_WBC); a.units = at<const int4>(p, mpc_plan::B_UNITS);
   a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
   a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
-  a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = 2 * p->nbmax;
-  a.up_off = d.up_off; a.up = d.up; a.down_off = d.down_off; a.down = d.down;
+  a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = p->nbmax;
   a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out;
-  a.row_base = d.row_base; a.rowcnt = d.rowcnt;
-  a.lo_f = d.lo_f; a.seg_hi = d.seg_hi; a.seg_lo = d.seg_lo; a.hscan = d.hscan; a.rpos = d.rpos;
+  a.row_base = d.row_base; a.rowcnt = d.rowcnt; a.lo_f = d.lo_f; a.hiR = d.hiR;
   a.rows = d.rows; a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.cs = d.cs;
   return a;
 }
 
-// One launch clears every accumulator of a run (status, bitmaps, tallies).
+static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
+  (void)p;
+  FlankArgs a;
+  a.status = d.status; a.sample = d.sample; a.n_of = d.n_of; a.gbase = d.gbase;
+  a.tstart = d.tstart; a.i_end = d.i_end;
+  a.up_off = d.up_off; a.up = d.up; a.down_off = d.down_off; a.down = d.down;
+  a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out; a.rpos = d.rpos;
+  a.row_base = d.row_base; a.lo_f = d.lo_f; a.hiR = d.hiR; a.loR = d.loR;
+  a.rows = d.rows; a.N = d.N; a.read_offset = d.read_offset;
+  return a;
+}
+
+// One launch clears every accumulator of a run (status, bitmaps, tallies, rows).
 struct ClearArgs {
-  uint32_t* ptr[12];
-  int64_t words[12];
-  uint32_t value[12];
+  uint32_t* ptr[16];
+  int64_t words[16];
+  uint32_t value[16];
   int32_t n;
 };
 __global__ __launch_bounds__(256) void K_clear(ClearArgs c) {
@@ -1490,6 +1818,17 @@ static inline unsigned nblk(int64_t n, int b = 256) {
 extern "C" {
 
 int mpc_version(void) { return MPC_ABI_VERSION; }
+#ifdef MPC_PROF_PARSE
+int mpc_prof_parse(unsigned long long* out, int reset) {
+  HIPCHK(hipDeviceSynchronize());
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16));
+  if (reset) {
+    unsigned long long z[16] = {0};
+    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
+  }
+  return MPC_OK;
+}
+#endif
 const char* mpc_last_error(void) { return g_err.c_str(); }
 
 int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
@@ -1523,8 +1862,9 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   if (p->G >= (1ll << 30)) { delete p; return fail(MPC_E_ARG, "too many positions"); }
   if (p->Ng >= (1ll << 30)) { delete p; return fail(MPC_E_ARG, "too many reads (event words hold 30-bit read indices)"); }
   p->row_cap = row_cap > 0 ? row_cap : 1;
+  if (p->row_cap >= (1ll << 31)) { delete p; return fail(MPC_E_ARG, "row capacity must be < 2^31"); }
   p->runs_cap = p->Ng + p->G;
-  p->ins_cap = in->cs_bytes / 2 + 3 * p->N + 16;  // insertions + 2 flank events per read
+  p->ins_cap = in->cs_bytes / 2 + 3 * p->N + 16;  // insertions (>= 2 cs bytes each) + slack per read
   p->ovf_cap = in->cs_bytes / 6 + 16;
   int eb = 1;
   while ((1ll << eb) <= p->G + 1) ++eb;
@@ -1561,29 +1901,15 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     for (int s = 0; s < p->S; ++s) {
       const int nb = (int)((p->ref_len[s] + 1 + kBW - 1) / kBW);
       if (pw_begin[s + 1] == pw_begin[s]) continue;  // no reads: nothing to tally
-      for (int b = 0; b < 2 * nb; ++b)  // insertion buckets, then flank buckets
+      for (int b = 0; b < nb; ++b)  // insertion buckets
         for (int c = pw_begin[s]; c < pw_begin[s + 1]; c += 256)
           p->work_bc.insert(p->work_bc.end(), {s, b, c, std::min(c + 256, pw_begin[s + 1])});
     }
     p->n_bc = (int64_t)(p->work_bc.size() / 4);
     p->units_cap = p->ins_cap / kUnit + p->n_bc + 1;
   }
-  {
-    size_t t = 0;
-    (void)hipcub::DeviceRadixSort::SortPairs(nullptr, t, (uint32_t*)nullptr, (uint32_t*)nullptr, (int32_t*)nullptr,
-                                             (int32_t*)nullptr, (int)std::max<int64_t>(p->Ng, 1), 0, eb);
-    size_t mx = t;
-    t = 0;
-    (void)hipcub::DeviceScan::InclusiveSum(nullptr, t, (int32_t*)nullptr, (int32_t*)nullptr, (int)p->runs_cap);
-    mx = std::max(mx, t);
-    t = 0;
-    (void)hipcub::DeviceScan::InclusiveSum(nullptr, t, (int32_t*)nullptr, (int32_t*)nullptr, (int)p->G);
-    mx = std::max(mx, t);
-    t = 0;
-    (void)hipcub::DeviceScan::ExclusiveSum(nullptr, t, (int32_t*)nullptr, (int32_t*)nullptr, (int)p->row_cap);
-    p->cub_tmp = std::max(mx, t);
-  }
   const int64_t N = p->N, Ng = p->Ng, G = p->G, R = p->row_cap, RU = p->runs_cap;
+  const int64_t nbg = (G + kGB - 1) / kGB, nbk = (R + kKB - 1) / kKB;
   auto set = [&](int b, int64_t count, size_t elem) { p->cnt[b] = count; p->sz[b] = (size_t)std::max<int64_t>(count, 1) * elem; };
   set(mpc_plan::B_STATUS, MPC_ST_WORDS, 4);
   set(mpc_plan::B_NOF, p->S, 4);
@@ -1591,17 +1917,22 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_IEND, N, 4);
   set(mpc_plan::B_INSRAW, p->ins_cap, 8);
   set(mpc_plan::B_INSSORT, p->ins_cap, 8);
-  set(mpc_plan::B_BKCNT, (int64_t)p->n_parse_wg * 2 * p->nbmax, 4);
-  set(mpc_plan::B_BKOFF, (int64_t)p->n_parse_wg * 2 * p->nbmax, 4);
+  set(mpc_plan::B_BKCNT, (int64_t)p->n_parse_wg * p->nbmax, 4);
+  set(mpc_plan::B_BKOFF, (int64_t)p->n_parse_wg * p->nbmax, 4);
   set(mpc_plan::B_RBASE, p->n_parse_wg, 8);
   set(mpc_plan::B_OVF, p->ovf_cap, sizeof(Ovf));
   set(mpc_plan::B_OVFCNT, 1, 4);
   set(mpc_plan::B_HASLEFT, (G + 31) / 32 + 1, 4);
   set(mpc_plan::B_MAXR, G, 4);
-  set(mpc_plan::B_KIN, Ng, 4);
-  set(mpc_plan::B_VIN, Ng, 4);
-  set(mpc_plan::B_KOUT, Ng, 4);
-  set(mpc_plan::B_VOUT, Ng, 4);
+  const int64_t nrb = (N + kRS - 1) / kRS;
+  set(mpc_plan::B_KIN, N, 4);
+  set(mpc_plan::B_VIN, N, 4);
+  set(mpc_plan::B_KOUT, N, 4);
+  set(mpc_plan::B_VOUT, N, 4);
+  set(mpc_plan::B_KTMP, N, 4);
+  set(mpc_plan::B_VTMP, N, 4);
+  set(mpc_plan::B_BCNT, nrb + 1, 4);
+  set(mpc_plan::B_BPRE, nrb + 1, 4);
   set(mpc_plan::B_RLEN, Ng, 4);
   set(mpc_plan::B_RPOS, N > 0 ? N : 1, 4);
   set(mpc_plan::B_RSTART, G + 1, 4);
@@ -1612,28 +1943,24 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_DIFF, G, 4);
   set(mpc_plan::B_SUB, G * 4, 4);
   set(mpc_plan::B_M, RU, 4);
-  set(mpc_plan::B_HFLAG, RU, 4);
-  set(mpc_plan::B_HSCAN, RU, 4);
-  set(mpc_plan::B_SEGR, RU, 4);
-  set(mpc_plan::B_SEGLO, RU, 4);
-  set(mpc_plan::B_SEGHI, RU, 4);
-  set(mpc_plan::B_SEGRUN, RU, 4);
+  set(mpc_plan::B_RUNR, RU, 4);
+  set(mpc_plan::B_HIR, RU, 4);
+  set(mpc_plan::B_LOR, RU, 4);
   set(mpc_plan::B_LOF, G, 4);
   set(mpc_plan::B_ROWCNT, G, 4);
   set(mpc_plan::B_ROWBASE, G, 4);
-  set(mpc_plan::B_DEPTH, G, 4);
+  set(mpc_plan::B_BSUM, 2 * nbg, 4);
   set(mpc_plan::B_ROWS, R * 4, 4);
-  set(mpc_plan::B_META, R, 1);
+  set(mpc_plan::B_META, (R + 3) / 4 * 4, 1);
   set(mpc_plan::B_RES, R * 4, 4);
-  set(mpc_plan::B_KEEP, R, 4);
-  set(mpc_plan::B_KEEPSCAN, R, 4);
+  set(mpc_plan::B_KEEP, nbk * 256, 4);
+  set(mpc_plan::B_KSUM, nbk, 4);
   set(mpc_plan::B_CALLS, R * 4, 4);
   set(mpc_plan::B_NCALLS, p->S + 1, 4);
   set(mpc_plan::B_MAXD, p->S, 4);
   set(mpc_plan::B_WPARSE, (int64_t)p->work_parse.size(), 4);
   set(mpc_plan::B_WBC, (int64_t)p->work_bc.size(), 4);
   set(mpc_plan::B_UNITS, p->units_cap * 4, 4);
-  set(mpc_plan::B_CUB, (int64_t)p->cub_tmp, 1);
   size_t o = 0;
   for (int b = 0; b < mpc_plan::B_COUNT; ++b) {
     o = (o + 255) & ~(size_t)255;
@@ -1666,6 +1993,8 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
   if (bytes < p->ws_bytes) return fail(MPC_E_WORKSPACE, "workspace too small");
   if (((uintptr_t)ws & 255) != 0) return fail(MPC_E_ARG, "workspace must be 256-byte aligned");
   if (((uintptr_t)p->in.cs & 15) != 0) return fail(MPC_E_ARG, "cs buffer must be 16-byte aligned");
+  if (((uintptr_t)p->in.up & 3) != 0 || ((uintptr_t)p->in.down & 3) != 0)
+    return fail(MPC_E_ARG, "flank buffers must be 4-byte aligned");
   p->ws = (uint8_t*)ws;
   HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_NOF), p->h_n.data(), 4 * p->S, hipMemcpyHostToDevice));
   HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_GBASE), p->h_gbase.data(), 4 * (p->S + 1), hipMemcpyHostToDevice));
@@ -1694,7 +2023,7 @@ int mpc_plan_buffer(const mpc_plan* p, int which, size_t* off, int64_t* count) {
     case MPC_BUF_HASLEFT: b = mpc_plan::B_HASLEFT; break;
     case MPC_BUF_MAXR: b = mpc_plan::B_MAXR; break;
     case MPC_BUF_RUN_M: b = mpc_plan::B_M; break;
-    case MPC_BUF_SEG_R: b = mpc_plan::B_SEGR; break;
+    case MPC_BUF_RUN_R: b = mpc_plan::B_RUNR; break;
     case MPC_BUF_DIFF: b = mpc_plan::B_DIFF; break;
     case MPC_BUF_SUB: b = mpc_plan::B_SUB; break;
     default: return fail(MPC_E_ARG, "unknown buffer");
@@ -1724,7 +2053,12 @@ int mpc_parse(mpc_plan* p, void* stream) {
     add(d.sub, 4 * p->G, 0u);
     add(d.maxR, p->G, 0u);
     add(d.maxdepth, p->S, 0u);
-    hipLaunchKernelGGL(K_clear, dim3(nblk(4 * p->G, 256) < 512 ? nblk(4 * p->G, 256) : 512), dim3(256), 0, st, c);
+    add(d.M, p->runs_cap, 0u);
+    add(d.runR, p->runs_cap, 0u);
+    add(d.rows, 4 * p->row_cap, 0u);
+    add(d.meta, (int64_t)(p->sz[mpc_plan::B_META] / 4), 0u);
+    const int64_t most = std::max<int64_t>(4 * p->row_cap, std::max<int64_t>(4 * p->G, p->runs_cap));
+    hipLaunchKernelGGL(K_clear, dim3(std::min<unsigned>(nblk(most, 256), 1024)), dim3(256), 0, st, c);
   }
   if (p->n_parse_wg > 0)
     launch_parse(p, d, st);
@@ -1736,15 +2070,10 @@ int mpc_index(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  if (p->N > 0) hipLaunchKernelGGL(K_rsplit, dim3(nblk(p->N)), dim3(256), 0, st, d, p->sentinel);
-  if (p->N > 0) {  // this shard's reads only: shards own contiguous read ranges
-    size_t tb = p->cub_tmp;
-    HIPCHK(hipcub::DeviceRadixSort::SortPairs(at<uint8_t>(p, mpc_plan::B_CUB), tb, d.keys_in, d.keys_out, d.vals_in,
-                                              d.vals_out, (int)p->N, 0, p->end_bit, st));
-  } else {
-    HIPCHK(hipMemsetAsync(d.keys_out, 0xff, 4, st));
-  }
-  hipLaunchKernelGGL(K_rstart, dim3(nblk(std::max<int64_t>(p->G + 1, p->N))), dim3(256), 0, st, d);
+  const int32_t nrb = (int32_t)((p->N + kRS - 1) / kRS);
+  if (p->N > 0) hipLaunchKernelGGL(K_rsplit, dim3(nrb), dim3(kRS), 0, st, d);
+  hipLaunchKernelGGL(K_rsort, dim3(1), dim3(kRS), 0, st, d, nrb, (int32_t)p->end_bit);
+  hipLaunchKernelGGL(K_rstart, dim3(nblk(std::max<int64_t>(p->G + 1, p->N))), dim3(256), 0, st, d);  // (M <= N)
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -1753,8 +2082,10 @@ int mpc_runs(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  if (p->n_shards > 1) hipLaunchKernelGGL(K_runs, dim3(1), dim3(1024), 0, st, d);
-  hipLaunchKernelGGL(K_zero_runs, dim3(nblk(p->runs_cap)), dim3(256), 0, st, d);
+  if (p->n_shards > 1) {
+    hipLaunchKernelGGL(K_runs, dim3(1), dim3(1024), 0, st, d);
+    if (p->N > 0) hipLaunchKernelGGL(K_runR, dim3(std::min<unsigned>(nblk(p->N), 1024)), dim3(256), 0, st, d);
+  }
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -1764,21 +2095,7 @@ int mpc_tally(mpc_plan* p, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
   if (p->n_bc > 0) hipLaunchKernelGGL(K_units, dim3(nblk(p->n_bc, 4)), dim3(256), 0, st, unit_args(p, d));
-  hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(256), 0, st, left_args(p, d));
-  HIPCHK(hipGetLastError());
-  return MPC_OK;
-}
-
-int mpc_segments(mpc_plan* p, void* stream) {
-  NEED_BOUND(p);
-  hipStream_t st = (hipStream_t)stream;
-  Dev d = p->dev();
-  uint8_t* tmp = at<uint8_t>(p, mpc_plan::B_CUB);
-  hipLaunchKernelGGL(K_seg_flags, dim3(nblk(p->runs_cap)), dim3(256), 0, st, d);
-  hipLaunchKernelGGL(K_seg_heads, dim3(nblk(p->G)), dim3(256), 0, st, d);
-  size_t tb = p->cub_tmp;
-  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, d.hflag, d.hscan, (int)p->runs_cap, st));
-  hipLaunchKernelGGL(K_seg_right, dim3(nblk(p->runs_cap)), dim3(256), 0, st, d);
+  hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -1787,11 +2104,7 @@ int mpc_layout(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  uint8_t* tmp = at<uint8_t>(p, mpc_plan::B_CUB);
-  hipLaunchKernelGGL(K_replay, dim3(nblk(p->G)), dim3(256), 0, st, d);
-  size_t tb = p->cub_tmp;
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, d.rowcnt, d.row_base, (int)p->G, st));
-  hipLaunchKernelGGL(K_rows_total, dim3(1), dim3(1), 0, st, d);
+  hipLaunchKernelGGL(K_replay, dim3(nblk(p->G, kGB)), dim3(kGB), 0, st, d);
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -1800,11 +2113,9 @@ int mpc_rows(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  uint8_t* tmp = at<uint8_t>(p, mpc_plan::B_CUB);
-  size_t tb = p->cub_tmp;
-  HIPCHK(hipcub::DeviceScan::InclusiveSum(tmp, tb, d.diff, d.depth, (int)p->G, st));
-  hipLaunchKernelGGL(K_assemble, dim3(nblk(p->G, 4)), dim3(256), 0, st, d);
-  hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(256), 0, st, flank_args(p, d));
+  hipLaunchKernelGGL(K_assemble, dim3(nblk(p->G, kGB)), dim3(kGB), 0, st, d);
+  hipLaunchKernelGGL(K_ins, dim3(ins_grid(p)), dim3(kUB), 0, st, ins_args(p, d));
+  if (p->N > 0) hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(256), 0, st, flank_args(p, d));
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -1817,11 +2128,8 @@ int mpc_consensus(mpc_plan* p, double mdf, double gtf, void* stream) {
   d.gtf = gtf;
   const int64_t R = p->row_cap;
   hipLaunchKernelGGL(K_call, dim3(nblk(R)), dim3(256), 0, st, d, R);
-  hipLaunchKernelGGL(K_keep, dim3(nblk(R)), dim3(256), 0, st, d, R);
-  uint8_t* tmp = at<uint8_t>(p, mpc_plan::B_CUB);
-  size_t tb = p->cub_tmp;
-  HIPCHK(hipcub::DeviceScan::ExclusiveSum(tmp, tb, d.keep, d.keep_scan, (int)R, st));
-  hipLaunchKernelGGL(K_emit, dim3(nblk(R)), dim3(256), 0, st, d, R);
+  hipLaunchKernelGGL(K_keep, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R);
+  hipLaunchKernelGGL(K_emit, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R);
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -1836,7 +2144,10 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
       launch_parse(p, d, st);
       break;
     case MPC_K_LEFT:
-      hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(256), 0, st, left_args(p, d));
+      hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));
+      break;
+    case MPC_K_INS:
+      hipLaunchKernelGGL(K_ins, dim3(ins_grid(p)), dim3(kUB), 0, st, ins_args(p, d));
       break;
     case MPC_K_FLANK:
       hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(256), 0, st, flank_args(p, d));
@@ -1854,7 +2165,6 @@ int mpc_run(mpc_plan* p, double mdf, double gtf, void* stream) {
   if ((rc = mpc_index(p, stream))) return rc;
   if ((rc = mpc_runs(p, stream))) return rc;
   if ((rc = mpc_tally(p, stream))) return rc;
-  if ((rc = mpc_segments(p, stream))) return rc;
   if ((rc = mpc_layout(p, stream))) return rc;
   if ((rc = mpc_rows(p, stream))) return rc;
   return mpc_consensus(p, mdf, gtf, stream);

@@ -15,7 +15,7 @@ phases it exchanges small arrays (no read data moves):
     after index     GATHER per-gap mixed RIGHT counts -> global run index space
                     MAX  maxR                     (RIGHT-only gaps)
     after tally     MAX  M per run                (longest LEFT string per run)
-    after segments  MAX  segR per segment         (longest RIGHT string per segment)
+                    MAX  runR per run             (length of the RIGHT string closing the run)
     after rows      SUM  rows                     (odd rows from shard 0, slot tallies from all)
 
 after which layout and consensus are identical on every shard.  The protocol
@@ -162,8 +162,7 @@ def exchange_step(plans, ex, mdf, gtf, stream=None):
     each("runs")
     each("tally")
     ex.reduce([p.buffer(eng.BUF_RUN_M, i32) for p in plans], "max")
-    each("segments")
-    ex.reduce([p.buffer(eng.BUF_SEG_R, i32) for p in plans], "max")
+    ex.reduce([p.buffer(eng.BUF_RUN_R, i32) for p in plans], "max")
     each("layout")
     each("rows")
     ex.reduce([p.buffer(eng.BUF_ROWS, i32) for p in plans], "sum")

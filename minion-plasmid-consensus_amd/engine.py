@@ -12,18 +12,18 @@ import numpy as np
 
 from . import _build
 
-LIB_PATH = _build.LIBMPC
+LIB_PATH = os.environ.get("MPC_LIB", _build.LIBMPC)  # override: experiments with library variants
 
-ABI_VERSION = 2
+ABI_VERSION = 3
 MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED = 0, 1, 2, 3
 DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL = 1, 2, 4, 8, 16, 32
 (BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_CNT, BUF_RIGHT_CNT_ALL,
- BUF_HASLEFT, BUF_MAXR, BUF_RUN_M, BUF_SEG_R, BUF_DIFF, BUF_SUB) = range(14)
-PHASES = ("parse", "index", "runs", "tally", "segments", "layout", "rows")
+ BUF_HASLEFT, BUF_MAXR, BUF_RUN_M, BUF_RUN_R, BUF_DIFF, BUF_SUB) = range(14)
+PHASES = ("parse", "index", "runs", "tally", "layout", "rows")
 
 DE_NAMES = {DE_OP: "Unknown operator", DE_VALUE: "ValueError", DE_INDEX: "IndexError", DE_KEY: "KeyError",
             DE_CAPACITY: "row capacity", DE_INTERNAL: "internal invariant"}
-K_PARSE, K_ODD, K_LEFT, K_FLANK = 0, 1, 2, 3
+K_PARSE, K_ODD, K_LEFT, K_FLANK, K_INS = 0, 1, 2, 3, 4
 CS_PAD = 2048  # readable bytes required past the end of the cs buffer (mpc.h)
 FLANK_PAD = 16  # readable bytes required past the end of the up/down buffers (mpc.h)
 

@@ -15,7 +15,7 @@ def declared():
 def test_header_declares_entry_points():
     names = declared()
     for f in ("mpc_version", "mpc_plan_create", "mpc_plan_bind", "mpc_parse", "mpc_index", "mpc_runs", "mpc_tally",
-              "mpc_segments", "mpc_layout", "mpc_rows", "mpc_consensus", "mpc_run", "mpc_profile_kernel"):
+              "mpc_layout", "mpc_rows", "mpc_consensus", "mpc_run", "mpc_profile_kernel"):
         assert f in names
 
 
@@ -25,7 +25,7 @@ def test_library_exports_all(pkg):
     for name in declared():
         assert hasattr(lib, name), name
     lib.mpc_version.restype = ctypes.c_int
-    assert lib.mpc_version() == pkg.engine.ABI_VERSION == 2
+    assert lib.mpc_version() == pkg.engine.ABI_VERSION == 3
 
 
 def test_no_oracle_in_product():

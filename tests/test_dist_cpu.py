@@ -37,7 +37,7 @@ class FakePlan:
             eng.BUF_HASLEFT: i((G + 31) // 32 + 1, hi=2 ** 30),
             eng.BUF_DIFF: i(G), eng.BUF_SUB: i(4 * G),
             eng.BUF_RIGHT_CNT: i(G, hi=50), eng.BUF_RIGHT_CNT_ALL: torch.zeros(n_shards * G, dtype=torch.int32),
-            eng.BUF_MAXR: i(G), eng.BUF_RUN_M: i(G + 11), eng.BUF_SEG_R: i(G + 11),
+            eng.BUF_MAXR: i(G), eng.BUF_RUN_M: i(G + 11), eng.BUF_RUN_R: i(G + 11),
             eng.BUF_ROWS: i(4 * ROWS),
         }
         self.initial = {k: v.clone() for k, v in self.buf.items()}
@@ -56,7 +56,7 @@ def expected(n_shards):
     init = [p.initial for p in plans]
     out = {}
     for b, op in ((eng.BUF_HASLEFT, "or"), (eng.BUF_DIFF, "sum"), (eng.BUF_SUB, "sum"), (eng.BUF_MAXR, "max"),
-                  (eng.BUF_RUN_M, "max"), (eng.BUF_SEG_R, "max"), (eng.BUF_ROWS, "sum")):
+                  (eng.BUF_RUN_M, "max"), (eng.BUF_RUN_R, "max"), (eng.BUF_ROWS, "sum")):
         acc = init[0][b].clone()
         for x in init[1:]:
             acc = acc + x[b] if op == "sum" else (acc.maximum(x[b]) if op == "max" else acc | x[b])
@@ -65,7 +65,7 @@ def expected(n_shards):
     return out
 
 
-PHASES = ["parse", "index", "runs", "tally", "segments", "layout", "rows", "consensus"]
+PHASES = ["parse", "index", "runs", "tally", "layout", "rows", "consensus"]
 
 
 def test_local_exchange_combines():

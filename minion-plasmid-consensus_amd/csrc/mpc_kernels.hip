@@ -26,6 +26,7 @@
 #include <algorithm>
 #include <cstdio>
 #include <cstring>
+#include <cstdlib>
 #include <string>
 #include <vector>
 
@@ -41,9 +42,8 @@ constexpr uint32_t DE_OP = MPC_DE_OP, DE_VALUE = MPC_DE_VALUE, DE_INDEX = MPC_DE
 
 constexpr int kBlk = 1024;          // cs bytes staged per wave iteration (64 lanes x 16 B)
 constexpr int kInsInline = 4;       // insertions up to this length travel as one event word
-constexpr int kMaxRefLen = (1 << 22) - 1;
-constexpr int kAdvCap = 1 << 22;    // > any reference length: a clamped advance keeps i past the end
-constexpr int kLaneCap = 1 << 24;   // saturation of one lane's advance sum (64 lanes stay < 2^31)
+constexpr int kMaxRefLen = (1 << 20) - 2;  // 32-bit coordinates: advances are clamped at kAdvCap > n
+constexpr int kAdvCap = 1 << 20;    // > any reference length: a clamped advance keeps i past the end
 constexpr int kICap = 1 << 28;      // saturation of the running coordinate i
 constexpr int kBW = 16;             // gaps per insertion bucket (K_left workgroup)
 constexpr int kKMax = 8;            // runs per gap tallied in K_left's LDS (others go to HBM)
@@ -143,24 +143,21 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int j) {
 // ---------------------------------------------------------------------------
 // K_parse: Step 4 of the reference (:285-323 tokenizer, :74-104 processOperation)
 // ---------------------------------------------------------------------------
-constexpr int kPW = 8;                  // waves per workgroup
-constexpr int kWin = 1024;              // window bytes (64 lanes x 16 B)
-constexpr int kStage = kWin + 128;      // + operand lookahead (halo, lanes 0..7)
-constexpr int kChunks = kStage / 16;
-constexpr int kHaloLanes = (kStage - kWin) / 16;
 constexpr int kSlots = 64;              // reads touching a window (slot 0 = read carried in)
-constexpr int kIB = 96;                 // staged insertion events per wave
-constexpr uint32_t kNoEnd = 0x7fffu;    // sentinel: next boundary lies beyond the halo
+constexpr int kMaxPW = 16;              // waves per workgroup (runtime: blockDim.x / 64)
+constexpr uint32_t kFar = 0x7fffu;      // sentinel: the window's only token ends beyond the window
 
-struct WaveLds {                        // per-wave LDS of K_parse
-  int64_t s_val[kSlots];                // i = s_val + (window prefix of advances)
+template <int WIN>
+struct alignas(16) WaveLds {            // per-wave LDS of K_parse
+  int32_t s_val[kSlots];                // i = s_val + (window prefix of advances)
+  int32_t s_ts[kSlots];                 // tstart (clamped; -1: negative)
+  int32_t s_read[kSlots];               // local read index
+  int32_t s_iend[kSlots];               // i_end | bit 30: read has a downstream flank
   int64_t s_end[kSlots];                // cs offset of the read's end
-  uint64_t ibuf[kIB];
-  int32_t s_ts[kSlots], s_read[kSlots], s_iend[kSlots];  // s_iend bit 30: read has a downstream flank
-  uint8_t stage[kStage + 16];           // window + halo (+16: aligned word reads past the end)
-  uint16_t em[kChunks];                 // boundary bits: special characters | read starts
-  uint16_t ra[kChunks];                 // read-start bits
-  uint16_t tok[kWin + 2];               // token starts in [P, E), then the sentinel; bit 15 = read start
+  uint8_t stage[WIN + 16];              // window bytes (+16: word reads past the end)
+  uint8_t em[WIN / 8];                  // boundary bits (special characters | read starts), bit = byte
+  uint8_t ra[WIN / 8];                  // read-start bits
+  uint16_t tok[WIN + 2];                // token starts in [P, C), then the sentinel C; bit 15 = read start
 };
 
 struct ParseArgs {  // slim argument block (no SGPR spills)
@@ -168,25 +165,27 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
   const int64_t* up_off; const int64_t* down_off; const int32_t* n_of; const int32_t* gbase;
   const int4* work;  // per workgroup: {sample, first read, end read, 0}
   int64_t cs_base, ovf_cap, read_offset, n_reads;
-  int32_t fused, nbs;  // nbs: bucket slots per parse workgroup (2 x max buckets)
+  int32_t nbs;       // bucket slots per parse workgroup (max buckets)
   int32_t* i_end; uint64_t* ins_raw; uint64_t* ins_sorted; int32_t* bk_cnt; int32_t* bk_off; int64_t* rbase;
   Ovf* ovf; uint32_t* ovf_cnt; uint32_t* hasleft; uint32_t* status;
   int32_t* diff; uint32_t* sub;
 };
 
-__host__ __device__ constexpr int parse_stage_bytes() { return kPW * (int)sizeof(WaveLds) + 16; }
 __host__ __device__ inline int parse_hl_words(int n) { return (n + 1 + 31) / 32; }
-__host__ __device__ inline int parse_lds_bytes(int n_max, bool fused, int nbmax) {
-  const int tallies = fused ? 12 * (n_max + 1) : 0;
-  const int buckets = 16 * nbmax;  // counts + cursors, insertion and flank buckets
-  return parse_stage_bytes() + 4 * parse_hl_words(n_max) + (tallies > buckets ? tallies : buckets);
+__host__ __device__ constexpr int parse_misc_bytes() { return kMaxPW * 4 + kMaxPW * 8; }
+template <int WIN>
+__host__ __device__ inline int parse_lds_bytes(int n_max, bool fused, int nbmax, int nw) {
+  const int tallies = fused ? 12 * (n_max + 1) : 0;  // sub 4 x u16, deletion/span starts | ends u16
+  const int buckets = 8 * nbmax + 4 * (kMaxPW + 2);  // counts + cursors + per-wave prefix
+  return nw * (int)sizeof(WaveLds<WIN>) + parse_misc_bytes() + 4 * parse_hl_words(n_max) +
+         (tallies > buckets ? tallies : buckets);
 }
 
 struct TokInfo { int adv; int kind; uint32_t pay; uint32_t err; };
 
 // Semantics of one token that do not depend on its coordinate, operand read
-// from HBM: the slow path for rare tokens (operand past the staged halo, long
-// insertions, ':' operands that are not 1-4 plain digits).
+// from HBM: the slow path for rare tokens (a token longer than the window,
+// long insertions / substitution operands, ':' operands that are not 1-4 plain digits).
 __device__ TokInfo analyze_long(const uint8_t* cs, int64_t s, int64_t e, bool is_last) {
   TokInfo r{0, 0, 0u, 0u};
   const uint32_t op = cs[s];
@@ -216,13 +215,22 @@ __device__ TokInfo analyze_long(const uint8_t* cs, int64_t s, int64_t e, bool is
   return r;
 }
 
-// first special character in cs[x0, bound) (x0 16-aligned), else bound
-__device__ int64_t scan_special(const uint8_t* cs, int64_t x0, int64_t bound) {
-  for (int64_t x = x0; x < bound; x += 16) {
-    const uint4 v = *reinterpret_cast<const uint4*>(cs + x);
-    const int64_t lim = bound - x;
-    const uint32_t m = special_mask16(v, 0, lim > 16 ? 16 : (int)lim);
-    if (m) return x + __ffs(m) - 1;
+// first special character in cs[x0, bound) (x0 16-aligned), else bound: all lanes, 1 KiB per step
+__device__ int64_t scan_special_wave(const uint8_t* cs, int64_t x0, int64_t bound) {
+  for (int64_t x = x0; x < bound; x += 1024) {
+    const int64_t y = x + 16 * lane();
+    uint32_t m = 0;
+    if (y < bound) {
+      const uint4 v = *reinterpret_cast<const uint4*>(cs + y);
+      const int64_t lim = bound - y;
+      m = special_mask16(v, 0, lim > 16 ? 16 : (int)lim);
+    }
+    const uint64_t b = ballot(m != 0);
+    if (b) {
+      const int f = __ffsll((unsigned long long)b) - 1;
+      const uint32_t mf = (uint32_t)__builtin_amdgcn_readlane((int)m, f);
+      return x + 16 * f + __ffs(mf) - 1;
+    }
   }
   return bound;
 }
@@ -249,26 +257,39 @@ __device__ __forceinline__ void wave_sync_lds() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// inclusive wave prefix sum of values < 2^27 as int64 (two 32-bit DPP scans)
-__device__ __forceinline__ int64_t wave_scan_i64s(int v) {
-  const int lo = wave_scan_i32(v & 0xffff);
-  const int hi = wave_scan_i32(v >> 16);
-  return ((int64_t)hi << 16) + lo;
+__device__ __forceinline__ int lanes_below(uint64_t m) {
+  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// One window's prefetched inputs: 16 cs bytes per lane (+16 halo bytes on
-// lanes < kHaloLanes) and the offsets / tstart of reads rs0 + lane.
+// special-character bits of a lane's 8 staged bytes
+__device__ __forceinline__ uint32_t special_mask8(uint2 v) {
+  const uint32_t w[2] = {v.x, v.y};
+  uint32_t m = 0;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    const bool sp = (c == 0x3Au) | (c == 0x5Au) | (((c - 0x2Au) <= 3u) & (c != 0x2Cu));  // : Z * + -
+    m |= (uint32_t)sp << k;
+  }
+  return m;
+}
+
+// One window's prefetched inputs: WIN/64 cs bytes per lane and the offsets /
+// tstart of reads rs0 + lane.
+template <int CH> struct Chunk;
+template <> struct Chunk<16> { using T = uint4; };
+template <> struct Chunk<8> { using T = uint2; };
+template <int CH>
 struct WinIn {
-  uint4 d, h;
+  typename Chunk<CH>::T d;
   int64_t o, uo, dno;
   int32_t ts;
 };
-__device__ __forceinline__ WinIn fetch_window(const ParseArgs& a, int64_t P, int64_t rs0, int l) {
-  WinIn f;
+template <int CH>
+__device__ __forceinline__ WinIn<CH> fetch_window(const ParseArgs& a, int64_t P, int64_t rs0, int l) {
+  WinIn<CH> f;
   const int64_t A = P & ~(int64_t)15;
-  f.d = *reinterpret_cast<const uint4*>(a.cs + A + 16 * l);
-  f.h = make_uint4(0, 0, 0, 0);
-  if (l < kHaloLanes) f.h = *reinterpret_cast<const uint4*>(a.cs + A + kWin + 16 * l);
+  f.d = *reinterpret_cast<const typename Chunk<CH>::T*>(a.cs + A + CH * l);
   const int64_t r = rs0 + l;
   const bool ok = r <= a.n_reads;
   f.o = ok ? a.cs_off[r] : INT64_MAX;
@@ -277,23 +298,25 @@ __device__ __forceinline__ WinIn fetch_window(const ParseArgs& a, int64_t P, int
   f.ts = r < a.n_reads ? a.tstart[r] : 0;
   return f;
 }
-
-__device__ __forceinline__ int lanes_below(uint64_t m) {
-  return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-}
+__device__ __forceinline__ uint32_t chunk_mask(uint4 v) { return special_mask16(v, 0, 16); }
+__device__ __forceinline__ uint32_t chunk_mask(uint2 v) { return special_mask8(v); }
+__device__ __forceinline__ void chunk_store(uint8_t* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
+__device__ __forceinline__ void chunk_store(uint8_t* p, uint2 v) { *reinterpret_cast<uint2*>(p) = v; }
 
 // Workgroup = contiguous reads of ONE sample (host work table); wave w takes
-// the w-th eighth of them and streams their cs bytes in windows of 1 KiB
-// (16 B per lane, coalesced; the next window is loaded while this one is
+// the w-th part of them and streams their cs bytes in windows of WIN bytes
+// (WIN/64 per lane, coalesced; the next window is loaded while this one is
 // processed).  Token boundaries (special characters and read starts) are bits
-// of an LDS mask; the token starts of a window are compacted into a list and
-// processed ONE TOKEN PER LANE, 64 per round: a mostly branch-free decode of the
-// operand word, one DPP scan of the advances for the coordinates i (reads are
-// segments: per-read bases in a slot table), ballot/mbcnt for the read slot and
-// the insertion-event index.  Effects: substitution / deletion / span tallies
-// (LDS), insertion events (per-wave LDS ring), LEFT-gap bits (LDS bitmap); no
-// global store inside the rounds.  Epilogue: flush tallies, bucket-sort
-// insertion events by gap.
+// of an LDS mask.  A window is cut at its LAST boundary C, so every token in
+// [P, C) ends inside the window (no lookahead halo); the next window starts at
+// C.  The token starts are compacted into a list and processed ONE TOKEN PER
+// LANE, 64 per round: branch-free SWAR decode of the operand word, one DPP
+// scan of the advances for the coordinates i (reads are segments: per-read
+// bases in a slot table), ballot/mbcnt for the read slot and the insertion
+// event index.  Effects: substitution / deletion / span tallies (LDS, 12 B per
+// position), insertion events (stored straight into the wave's region of
+// ins_raw), LEFT-gap bits (LDS bitmap).  Epilogue: flush tallies, bucket-sort
+// the insertion events by gap.
 #ifdef MPC_PROF_PARSE
 // instrumentation build only: per-section shader cycles of K_parse summed over waves
 __device__ unsigned long long g_prof[16];
@@ -304,68 +327,62 @@ __device__ unsigned long long g_prof[16];
 #define PROF_ADD(k, v)
 #endif
 
-template <bool FUSED>
-__global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
+template <bool FUSED, int WIN>
+__global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
+  constexpr int CH = WIN / 64;
+  using WL = WaveLds<WIN>;
+  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
+  const int l = lane();
+  const int nw = (int)(blockDim.x >> 6);
+  const int w = uniform_i32((int)(threadIdx.x >> 6));
 #ifdef MPC_PROF_PARSE
   unsigned long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
   PROF_T(tk0);
 #endif
-  extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
-  const int l = lane();
-  const int w = uniform_i32((int)(threadIdx.x >> 6));
-  WaveLds& W = *reinterpret_cast<WaveLds*>(lds + w * (int)sizeof(WaveLds));
-  uint32_t* misc = reinterpret_cast<uint32_t*>(lds + parse_stage_bytes() - 16);  // [0] WG event count
+  WL& W = *reinterpret_cast<WL*>(lds + w * (int)sizeof(WL));
+  uint32_t* wcnt = reinterpret_cast<uint32_t*>(lds + nw * (int)sizeof(WL));     // [kMaxPW] events per wave
+  int64_t* wbase = reinterpret_cast<int64_t*>(wcnt + kMaxPW);                  // [kMaxPW] event region per wave
+  uint32_t* hl = reinterpret_cast<uint32_t*>(wbase + kMaxPW);                  // LEFT gaps bitmap
   const int4 wk = a.work[blockIdx.x];
   const int smp = wk.x;
   const int64_t r0 = wk.y, r1 = wk.z;
   const int n = a.n_of[smp];
   const int gb = a.gbase[smp];
-  uint32_t* hl = reinterpret_cast<uint32_t*>(lds + parse_stage_bytes());       // LEFT gaps bitmap
-  uint8_t* uni = lds + parse_stage_bytes() + 4 * parse_hl_words(n);
-  uint32_t* sub_l = reinterpret_cast<uint32_t*>(uni);                          // [2*(n+1)] 4 x u16
-  int32_t* diff_l = reinterpret_cast<int32_t*>(sub_l + 2 * (n + 1));           // [n+1]
-  constexpr bool fused = FUSED;  // tallies in LDS (one address space per instantiation)
-  const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;               // event region
-  const int64_t rb_cap = (a.cs_off[r1] - a.cs_base) / 2 + 3 * r1 - rb_wg;
+  uint32_t* uni = hl + parse_hl_words(n);
+  uint32_t* sub_l = uni;                // [2 (n+1)]: A | T << 16, C | G << 16
+  uint32_t* del_l = uni + 2 * (n + 1);  // [n+1]: depth-decrement count | depth-increment count << 16
+  constexpr bool fused = FUSED;         // tallies in LDS (one address space per instantiation)
   for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) hl[k] = 0;
   if (fused)
-    for (int k = threadIdx.x; k < 3 * (n + 1); k += blockDim.x) sub_l[k] = 0;
-  if (threadIdx.x == 0) misc[0] = 0;
+    for (int k = threadIdx.x; k < 3 * (n + 1); k += blockDim.x) uni[k] = 0;
   __syncthreads();
 
   auto odd_sub = [&](int pos, int code) {
     if (fused) atomicAdd(sub_l + 2 * pos + (code >> 1), 1u << (16 * (code & 1)));
     else atomicAdd(a.sub + (int64_t)(gb + pos) * 4 + code, 1u);
   };
-  auto odd_diff = [&](int pos, int v) {
-    if (fused) atomicAdd(diff_l + pos, v);
-    else atomicAdd(a.diff + gb + pos, v);
+  auto depth_dec = [&](int pos) {  // diff[pos] -= 1
+    if (fused) atomicAdd(del_l + pos, 1u);
+    else atomicAdd(a.diff + gb + pos, -1);
   };
-  int nib = 0;  // staged insertion events of this wave (wave-uniform)
-  auto flush_ibuf = [&]() {
-    wave_sync_lds();
-    int basepos = 0;
-    if (l == 0) basepos = (int)atomicAdd(misc, (uint32_t)nib);
-    basepos = __shfl(basepos, 0, 64);
-    if (basepos + nib > rb_cap) {
-      if (l == 0) atomicOr(&a.status[MPC_ST_FLAGS], DE_INTERNAL);
-    } else {
-      for (int k = l; k < nib; k += 64) a.ins_raw[rb_wg + basepos + k] = W.ibuf[k];
-    }
-    nib = 0;
+  auto depth_inc = [&](int pos) {  // diff[pos] += 1
+    if (fused) atomicAdd(del_l + pos, 1u << 16);
+    else atomicAdd(a.diff + gb + pos, 1);
   };
 
-  const int64_t ra = r0 + (r1 - r0) * w / kPW, rb = r0 + (r1 - r0) * (w + 1) / kPW;
+  const int64_t ra = r0 + (r1 - r0) * w / nw, rb = r0 + (r1 - r0) * (w + 1) / nw;
   const int64_t wend = a.cs_off[rb];
   int64_t P = a.cs_off[ra];
+  const int64_t ev_base = (P - a.cs_base) / 2 + 3 * ra;  // this wave's event region in ins_raw
+  uint32_t nev = 0;                                       // events written (wave-uniform)
   int64_t rs0 = ra;         // first read whose cs starts at or after P
   bool carry = false;       // slot 0 holds a read continuing into this window
-  WinIn cur = fetch_window(a, P, rs0, l);
+  WinIn<CH> cur = fetch_window<CH>(a, P, rs0, l);
   while (P < wend) {
     PROF_T(tw0);
     const int64_t A = P & ~(int64_t)15;
-    // ---- window end: at most 63 read starts in [P, E) ----
-    int64_t E = A + kWin < wend ? A + kWin : wend;
+    // ---- window: at most 63 read starts in [P, E) ----
+    int64_t E = A + WIN < wend ? A + WIN : wend;
     const int64_t o63 = readlane64(cur.o, 63);
     if (o63 < E) E = o63;
     const int64_t o_nx = __shfl(cur.o, (l + 1) & 63, 64);
@@ -378,22 +395,60 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
         a.i_end[rs0 + l] = cur.ts < 0 ? 0 : (cur.ts > n ? n + 1 : cur.ts);
       }
       rs0 += 63;
-      cur = fetch_window(a, P, rs0, l);
+      cur = fetch_window<CH>(a, P, rs0, l);
       continue;
     }
-    const bool inwin = l < 63 && cur.o < E;  // read rs0+l starts in [P, E)
-    const int nst = __popcll(ballot(inwin));
-    // ---- stage bytes, boundary bits, per-read slots ----
-    *reinterpret_cast<uint4*>(W.stage + 16 * l) = cur.d;
-    W.em[l] = (uint16_t)special_mask16(cur.d, 0, 16);
-    W.ra[l] = 0;
-    if (l < kHaloLanes) {
-      *reinterpret_cast<uint4*>(W.stage + kWin + 16 * l) = cur.h;
-      W.em[64 + l] = (uint16_t)special_mask16(cur.h, 0, 16);
-      W.ra[64 + l] = 0;
+    // ---- stage bytes, boundary bits ----
+    chunk_store(W.stage + CH * l, cur.d);
+    const uint32_t spm = chunk_mask(cur.d);
+    if (CH == 16) reinterpret_cast<uint16_t*>(W.em)[l] = (uint16_t)spm; else W.em[l] = (uint8_t)spm;
+    if (CH == 16) reinterpret_cast<uint16_t*>(W.ra)[l] = 0; else W.ra[l] = 0;
+    wave_sync_lds();
+    {  // read-start bits of every read starting inside the window (incl. E)
+      const int64_t rel = cur.o - A;
+      if (rel >= 0 && rel < WIN) {
+        atomicOr(reinterpret_cast<uint32_t*>(W.em) + (rel >> 5), 1u << (rel & 31));
+        atomicOr(reinterpret_cast<uint32_t*>(W.ra) + (rel >> 5), 1u << (rel & 31));
+      }
     }
-    if (nib + 64 > kIB) flush_ibuf();
-    bool lflank = false;
+    wave_sync_lds();
+    const int64_t cA = A + CH * l;
+    const uint32_t cmask = CH == 16 ? 0xffffu : 0xffu;
+    const uint32_t em_own = (CH == 16 ? (uint32_t)reinterpret_cast<const uint16_t*>(W.em)[l] : (uint32_t)W.em[l]) & cmask;
+    const uint32_t ra_own = (CH == 16 ? (uint32_t)reinterpret_cast<const uint16_t*>(W.ra)[l] : (uint32_t)W.ra[l]) & cmask;
+    // ---- cut C: E if E is a boundary (a read start), else the last boundary in (P, E) ----
+    const bool e_rs = (E == wend) || (E == o63);
+    int64_t C;
+    bool c_rs;
+    bool far = false;
+    if (e_rs) { C = E; c_rs = true; }
+    else {
+      int lo = (int)(P + 1 - cA), hi = (int)(E - cA);
+      lo = lo < 0 ? 0 : (lo > CH ? CH : lo);
+      hi = hi < 0 ? 0 : (hi > CH ? CH : hi);
+      const uint32_t m = em_own & ((hi >= 32 ? 0xffffffffu : (1u << hi) - 1u)) & ~((1u << lo) - 1u);
+      const uint64_t b = ballot(m != 0);
+      if (b) {
+        const int f = 63 - __clzll((long long)b);
+        const uint32_t mf = (uint32_t)__builtin_amdgcn_readlane((int)m, f);
+        const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)ra_own, f);
+        const int k = 31 - __clz(mf);
+        C = A + CH * f + k;
+        c_rs = (rf >> k) & 1u;
+      } else {
+        // one token runs past the window: its end is the next special character
+        // or the next read start (the first read start after P)
+        const uint64_t bn = ballot(cur.o > P);
+        const int fo = bn ? __ffsll((unsigned long long)bn) - 1 : 63;
+        const int64_t bound = readlane64(cur.o, fo) < wend ? readlane64(cur.o, fo) : wend;
+        C = scan_special_wave(a.cs, A + WIN, bound);
+        c_rs = C == bound;
+        far = true;
+      }
+    }
+    const bool inwin = l < 63 && cur.o < C;  // read rs0+l starts in [P, C)
+    const int nst = __popcll(ballot(inwin));
+    // ---- per-read slots ----
     if (inwin) {
       const int q = l + 1;
       const int64_t up = uo_nx - cur.uo, dn = dno_nx - cur.dno;
@@ -403,40 +458,23 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       if (up > 0 && ts > n) derr |= DE_INDEX;         // leftIndel(2*i) past the end
       if (o_nx <= cur.o) derr |= DE_OP;               // processOperation('', '')
       if (derr) flag_read(a, derr, rs0 + l);
-      if (up > 0 && ts >= 0 && ts <= n) {
-        atomicOr(hl + (ts >> 5), 1u << (ts & 31));
-        lflank = true;
-      }
+      if (up > 0 && ts >= 0 && ts <= n) atomicOr(hl + (ts >> 5), 1u << (ts & 31));  // upstream flank: LEFT at gap tstart
       W.s_end[q] = o_nx;
       W.s_ts[q] = ts < 0 ? -1 : (ts > kICap ? kICap : ts);
       W.s_read[q] = (int32_t)(rs0 + l);
       W.s_iend[q] = (ts < 0 ? 0 : (ts > n ? n + 1 : ts)) | (dn > 0 ? 1 << 30 : 0);
     }
-    (void)lflank;  // upstream flank = LEFT event at gap tstart: only its gap bit (tallied per read later)
-    wave_sync_lds();
-    {  // read-start bits of every known start in the stage
-      const int64_t rel = cur.o - A;
-      if (rel >= 0 && rel < kStage) {
-        atomicOr(reinterpret_cast<uint32_t*>(W.em) + (rel >> 5), 1u << (rel & 31));
-        atomicOr(reinterpret_cast<uint32_t*>(W.ra) + (rel >> 5), 1u << (rel & 31));
-      }
-    }
     PROF_T(tw1);
     // ---- prefetch the next window ----
-    const int64_t Pn = E, rsn = rs0 + nst;
-    WinIn nxt;
-    if (Pn < wend) nxt = fetch_window(a, Pn, rsn, l);
-    wave_sync_lds();
-
-    // ---- token list: starts in [P, E) (bit 15 = read start), then the sentinel ----
-    const int64_t cA = A + 16 * l;
-    const uint32_t em_own = W.em[l];
-    const uint32_t ra_own = W.ra[l];
+    const int64_t Pn = C, rsn = rs0 + nst;
+    WinIn<CH> nxt;
+    if (Pn < wend) nxt = fetch_window<CH>(a, Pn, rsn, l);
+    // ---- token list: starts in [P, C) (bit 15 = read start), then the sentinel ----
     int T;
     {
-      int tlo = (int)(P - cA), thi = (int)(E - cA < 16 ? E - cA : 16);
-      tlo = tlo < 0 ? 0 : (tlo > 16 ? 16 : tlo);
-      thi = thi < 0 ? 0 : thi;
+      int tlo = (int)(P - cA), thi = (int)(C - cA);
+      tlo = tlo < 0 ? 0 : (tlo > CH ? CH : tlo);
+      thi = thi < 0 ? 0 : (thi > CH ? CH : thi);
       const uint32_t tm = em_own & ((1u << thi) - 1u) & ~((1u << tlo) - 1u);
       const int cnt = __popc(tm);
       const int incl = wave_scan_i32(cnt);
@@ -446,56 +484,38 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       while (m) {
         const int k = __ffs(m) - 1;
         m &= m - 1;
-        W.tok[idx++] = (uint16_t)((16 * l + k) | (((ra_own >> k) & 1u) << 15));
+        W.tok[idx++] = (uint16_t)((CH * l + k) | (((ra_own >> k) & 1u) << 15));
       }
-      // first boundary at or after E: ends the window's last token
-      const int sh = (int)(E - cA);
-      const uint32_t sb = sh >= 16 ? 0u : (sh <= 0 ? em_own : em_own & ~((1u << sh) - 1u));
-      uint64_t bal = ballot(sb != 0);
-      uint32_t sent = kNoEnd;
-      if (bal) {
-        const int f = __ffsll((unsigned long long)bal) - 1;
-        const uint32_t bf = (uint32_t)__builtin_amdgcn_readlane((int)sb, f);
-        const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)ra_own, f);
-        const int k = __ffs(bf) - 1;
-        sent = (uint32_t)(16 * f + k) | (((rf >> k) & 1u) << 15);
-      } else {
-        const uint32_t hb = l < kHaloLanes ? W.em[64 + l] : 0u;
-        const uint32_t hr = l < kHaloLanes ? W.ra[64 + l] : 0u;
-        bal = ballot(hb != 0);
-        if (bal) {
-          const int f = __ffsll((unsigned long long)bal) - 1;
-          const uint32_t bf = (uint32_t)__builtin_amdgcn_readlane((int)hb, f);
-          const uint32_t rf = (uint32_t)__builtin_amdgcn_readlane((int)hr, f);
-          const int k = __ffs(bf) - 1;
-          sent = (uint32_t)(kWin + 16 * f + k) | (((rf >> k) & 1u) << 15);
-        }
-      }
-      if (l == 0) W.tok[T] = (uint16_t)sent;
+      if (l == 0) W.tok[T] = far ? (uint16_t)(kFar | (c_rs ? 0x8000u : 0u)) : (uint16_t)((C - A) | (c_rs ? 0x8000u : 0u));
     }
     wave_sync_lds();
-
     PROF_T(tw2);
+
     // ---- rounds: one token per lane ----
-    int64_t G = 0;  // advances of the window's earlier rounds
+    int32_t G = 0;  // advances of the window's earlier rounds
     int qc = 0;     // read starts of the window's earlier rounds
     for (int t0 = 0; t0 < T; t0 += 64) {
-      if (nib + 64 > kIB) flush_ibuf();
       const int t = t0 + l;
       const bool v = t < T;
       const uint32_t e0 = v ? W.tok[t] : 0u, e1 = v ? W.tok[t + 1] : 0u;
       const int sx = (int)(e0 & 0x7fffu);
-      const int ex = (int)(e1 & 0x7fffu);
+      const bool lfar = v && ((e1 & 0x7fffu) == kFar);
+      const int64_t ex64 = lfar ? C - A : (int64_t)(e1 & 0x7fffu);  // far: the token ends at C (beyond the window)
+      const int ex = (int)(ex64 - sx - 1 < kAdvCap ? ex64 : sx + 1 + kAdvCap);
       const bool is_rs = v && (e0 >> 15);
-      bool last = v && (e1 >> 15);
+      const bool last = v && (e1 >> 15);
       const uint64_t brs = ballot(is_rs);
       const int q = qc + lanes_below(brs) + (is_rs ? 1 : 0);
-      // fast decode from the staged bytes
-      const uint32_t op = W.stage[sx];
-      const int ao = sx + 1;
+      // fast decode from the staged bytes: op, then 4 operand bytes
       const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage);
-      const uint32_t w0 = __builtin_amdgcn_alignbyte(b32[(ao >> 2) + 1], b32[ao >> 2], (uint32_t)(ao & 3));
-      int olen = ex - sx - 1;
+      const int a4 = sx >> 2;
+      const uint32_t sh = (uint32_t)(sx & 3);
+      const uint32_t d0 = b32[a4], d1 = b32[a4 + 1], d2 = b32[a4 + 2];
+      const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+      const uint32_t x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+      const uint32_t op = x0 & 0xffu;
+      const uint32_t w0 = __builtin_amdgcn_alignbyte(x1, x0, 1u);
+      const int olen = ex - sx - 1;
       // branch-free decode: op class, 4 operand bytes at once (SWAR)
       const bool colon = op == ':', star = op == '*', plus = op == '+', minus = op == '-';
       const bool spec = colon | star | plus | minus | (op == 'Z');
@@ -521,79 +541,71 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
       pk = (pk | (pk >> 6)) & 0x000f000fu;
       pk = (pk | (pk >> 12)) & 0xffu;
       uint32_t pay = star ? ((codes >> shl) & 3u) : (pk & ((1u << (2 * ol4)) - 1u));
-      bool slow = v & ((ex == (int)kNoEnd) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4)))));
+      const bool slow = lfar | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));
       int kind = !act ? 0 : colon ? (adv_c > 0 ? 1 : 0) : (olen <= 0) ? 0 : star ? 2 : plus ? 3 : minus ? 4 : 0;
       int adv = kind == 1 ? adv_c : kind == 2 ? 1 : kind == 4 ? (olen < kAdvCap ? olen : kAdvCap) : 0;
       uint32_t err = (v & !spec) ? DE_OP : 0u;  // cs does not start with an operator (:100-102)
       if (act & star & (olen == 0)) err |= DE_INDEX;  // operand[-1] of '' (:96)
       if ((kind == 2) & !last_ok) err |= DE_KEY;
       if ((kind == 3) & ((bad & vm) != 0)) err |= DE_KEY;
+      int olen_e = olen;
       if (slow) {  // rare: decode from HBM
-        const int64_t s = A + sx;
-        int64_t e = A + ex;
-        if (ex == (int)kNoEnd) {
-          const int64_t send = W.s_end[q];
-          e = scan_special(a.cs, A + kStage, send);
-          last = e == send;
-        }
+        const int64_t s = A + sx, e = A + ex64;
         const TokInfo ti = analyze_long(a.cs, s, e, last);
         adv = ti.adv; kind = ti.kind; pay = ti.pay; err = ti.err;
-        olen = (int)(e - s - 1 < kAdvCap ? e - s - 1 : kAdvCap);
+        olen_e = (int)(e - s - 1 < kAdvCap ? e - s - 1 : kAdvCap);
       }
       // ---- coordinates ----
-      const int ainc = wave_scan_i32(adv);  // adv <= 2^22: 64 lanes stay < 2^31
+      const int ainc = wave_scan_i32(adv);  // adv <= 2^20: 64 lanes stay < 2^31
       const int aex = ainc - adv;
       const int atot = wave_last_i32(ainc);
-      if (is_rs) W.s_val[q] = (int64_t)W.s_ts[q] - (G + aex);
+      if (is_rs) W.s_val[q] = W.s_ts[q] - (G + aex);
       wave_sync_lds();
-      const int64_t i64 = W.s_val[q] + G + aex;
-      const int itok = (int)(i64 < -(1 << 30) ? -(1 << 30) : (i64 > kICap ? kICap : i64));
+      const int i = W.s_val[q] + G + aex;
       // ---- effects ----
       uint32_t te = err;
-      if (kind == 1 && (int64_t)itok + adv > n) te |= DE_INDEX;
-      if (kind == 2 && itok >= n) te |= DE_INDEX;
-      if (kind == 3 && itok > n) te |= DE_INDEX;
-      const int64_t rl = W.s_read[q];
-      const bool ins_inline = kind == 3 && olen <= kInsInline;
-      const uint64_t bins = ballot(ins_inline);
+      if (kind == 1 && (i < 0 || i + adv > n)) te |= DE_INDEX;
+      if (kind == 2 && (uint32_t)i >= (uint32_t)n) te |= DE_INDEX;
+      if (kind == 3 && (uint32_t)i > (uint32_t)n) te |= DE_INDEX;
+      const int rl = W.s_read[q];
       if (te == 0) {
-        if (kind == 2) odd_sub(itok, (int)pay);
-        if (kind == 4 && itok >= 0 && itok < n) {
-          odd_diff(itok, -1);
-          odd_diff((int64_t)itok + olen < n ? itok + olen : n, 1);
+        if (kind == 2) odd_sub(i, (int)pay);
+        if (kind == 4 && i >= 0 && i < n) {
+          depth_dec(i);
+          depth_inc(i + olen_e < n ? i + olen_e : n);
         }
         if (kind == 3) {
-          atomicOr(hl + (itok >> 5), 1u << (itok & 31));
-          if (olen > kInsInline) push_ovf(a, A + sx + 1, rl, itok, olen);
+          atomicOr(hl + (i >> 5), 1u << (i & 31));
+          if (olen_e > kInsInline) push_ovf(a, A + sx + 1, rl, i, olen_e);
         }
       }
-      if (ins_inline)
-        W.ibuf[nib + lanes_below(bins)] = te == 0 ? ins_event(itok, olen, pay, a.read_offset + rl)
-                                                 : ins_event((int)kNullGap, 1, 0u, a.read_offset + rl);
+      const bool ins_inline = kind == 3 && olen_e <= kInsInline && te == 0;
+      const uint64_t bins = ballot(ins_inline);
+      if (ins_inline) a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);
       if (last) {  // the read's last operation: i_end, downstream check, span
-        const int64_t ia = i64 + adv;
-        const int ie = (int)(ia < 0 ? 0 : (ia > n ? n + 1 : ia));
+        const int ia = i + adv;
+        const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
         const int dnf = W.s_iend[q] & (1 << 30);
         if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
         W.s_iend[q] = ie | dnf;
         const int ts = W.s_ts[q];
         const int e2 = ie > n ? n : ie;
-        if (ts >= 0 && ts < e2) { odd_diff(ts, 1); odd_diff(e2, -1); }
+        if (ts >= 0 && ts < e2) { depth_inc(ts); depth_dec(e2); }
       }
       if (te) flag_read(a, te, rl);
       G += atot;
       qc += __popcll(brs);
-      nib += __popcll(bins);
+      nev += (uint32_t)__popcll(bins);
     }
     wave_sync_lds();
     PROF_T(tw3);
     PROF_ADD(0, tw1 - tw0); PROF_ADD(1, tw2 - tw1); PROF_ADD(2, tw3 - tw2); PROF_ADD(4, 1); PROF_ADD(5, (T + 63) / 64);
     // ---- reads that ended in this window: i_end; carry the open one ----
-    if (l <= nst && (l > 0 || carry) && W.s_end[l] <= E) a.i_end[W.s_read[l]] = W.s_iend[l] & ~(1 << 30);
-    const bool cont = (nst > 0 || carry) && W.s_end[nst] > E;
+    if (l <= nst && (l > 0 || carry) && W.s_end[l] <= C) a.i_end[W.s_read[l]] = W.s_iend[l] & ~(1 << 30);
+    const bool cont = (nst > 0 || carry) && W.s_end[nst] > C;
     if (cont && l == 0) {
-      const int64_t v = W.s_val[nst] + G;
-      W.s_val[0] = v > kICap ? kICap : v;
+      const int64_t v = (int64_t)W.s_val[nst] + G;
+      W.s_val[0] = (int32_t)(v > kICap ? kICap : v);
       W.s_end[0] = W.s_end[nst];
       W.s_ts[0] = W.s_ts[nst];
       W.s_read[0] = W.s_read[nst];
@@ -603,10 +615,10 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
     wave_sync_lds();
     P = Pn;
     rs0 = rsn;
+    if (Pn < wend) cur = nxt;
 #ifdef MPC_PROF_PARSE
     { PROF_T(tw4); PROF_ADD(3, tw4 - tw3); }
 #endif
-    if (Pn < wend) cur = nxt;
   }
   // reads starting at the range end have an empty cs
   for (int64_t r = rs0 + l; r < rb; r += 64) {
@@ -614,7 +626,7 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
     flag_read(a, DE_OP, r);
     a.i_end[r] = ts < 0 ? 0 : (ts > n ? n + 1 : ts);
   }
-  if (nib) flush_ibuf();
+  if (l == 0) { wcnt[w] = nev; wbase[w] = ev_base; }
 #ifdef MPC_PROF_PARSE
   {
     PROF_T(tk1);
@@ -624,20 +636,17 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
 #endif
   __syncthreads();
   // ---- flush LDS tallies and the LEFT-gap bitmap ----
-#ifdef MPC_EXP_NOFLUSH_PARSE
-  if (false) {
-#else
   if (fused) {
-#endif
     for (int p = threadIdx.x; p <= n; p += blockDim.x) {
-      const int32_t dv = diff_l[p];
+      const uint32_t dl = del_l[p];
+      const int32_t dv = (int32_t)(dl >> 16) - (int32_t)(dl & 0xffffu);
       if (dv) atomicAdd(a.diff + gb + p, dv);
-      const uint32_t w0 = sub_l[2 * p], w1 = sub_l[2 * p + 1];
+      const uint32_t s0 = sub_l[2 * p], s1 = sub_l[2 * p + 1];
       uint32_t* sg = a.sub + (int64_t)(gb + p) * 4;
-      if (w0 & 0xffffu) atomicAdd(sg + 0, w0 & 0xffffu);
-      if (w0 >> 16) atomicAdd(sg + 1, w0 >> 16);
-      if (w1 & 0xffffu) atomicAdd(sg + 2, w1 & 0xffffu);
-      if (w1 >> 16) atomicAdd(sg + 3, w1 >> 16);
+      if (s0 & 0xffffu) atomicAdd(sg + 0, s0 & 0xffffu);
+      if (s0 >> 16) atomicAdd(sg + 1, s0 >> 16);
+      if (s1 & 0xffffu) atomicAdd(sg + 2, s1 & 0xffffu);
+      if (s1 >> 16) atomicAdd(sg + 3, s1 >> 16);
     }
   }
   for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) {
@@ -650,25 +659,36 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   __syncthreads();
   // ---- bucket-sort this workgroup's insertion events by gap (counting sort) ----
   const int nbk = (n + 1 + kBW - 1) / kBW;
-  const int nbt = nbk;
-  uint32_t* bcnt = reinterpret_cast<uint32_t*>(uni);  // aliases the (flushed) tallies
-  uint32_t* bcur = bcnt + nbt;
-  const int Ev = (int)misc[0];
-  for (int k = threadIdx.x; k < nbt; k += blockDim.x) bcnt[k] = 0;
+  uint32_t* bcnt = uni;  // aliases the (flushed) tallies
+  uint32_t* bcur = bcnt + nbk;
+  int32_t* wpre = reinterpret_cast<int32_t*>(bcur + nbk);  // [kMaxPW + 1]
+  for (int k = threadIdx.x; k < nbk; k += blockDim.x) bcnt[k] = 0;
+  if (threadIdx.x == 0) {
+    int s = 0;
+    for (int k = 0; k < nw; ++k) { wpre[k] = s; s += (int)wcnt[k]; }
+    wpre[nw] = s;
+  }
   __syncthreads();
+  const int Ev = wpre[nw];
+  const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;
+  auto ev_src = [&](int k) {  // k-th event of the workgroup (wave regions in wave order)
+    int ww = 0;
+    while (ww + 1 < nw && wpre[ww + 1] <= k) ++ww;
+    return wbase[ww] + (k - wpre[ww]);
+  };
   for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
-    const uint64_t ev = a.ins_raw[rb_wg + k];
+    const uint64_t ev = a.ins_raw[ev_src(k)];
     const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
     if (gap <= (uint32_t)n) atomicAdd(bcnt + gap / kBW, 1u);
   }
   __syncthreads();
   if (threadIdx.x < 64) {  // exclusive scan over buckets by one wave
     int carry_b = 0;
-    for (int c0 = 0; c0 < nbt; c0 += 64) {
+    for (int c0 = 0; c0 < nbk; c0 += 64) {
       const int k = c0 + l;
-      const int v = k < nbt ? (int)bcnt[k] : 0;
+      const int v = k < nbk ? (int)bcnt[k] : 0;
       const int inc = wave_scan_i32(v);
-      if (k < nbt) {
+      if (k < nbk) {
         bcur[k] = (uint32_t)(carry_b + inc - v);
         a.bk_cnt[(int64_t)blockIdx.x * a.nbs + k] = v;
         a.bk_off[(int64_t)blockIdx.x * a.nbs + k] = carry_b + inc - v;
@@ -679,7 +699,7 @@ __global__ __launch_bounds__(kPW * 64) void K_parse(ParseArgs a) {
   if (threadIdx.x == 0) a.rbase[blockIdx.x] = rb_wg;
   __syncthreads();
   for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
-    const uint64_t ev = a.ins_raw[rb_wg + k];
+    const uint64_t ev = a.ins_raw[ev_src(k)];
     const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
     if (gap <= (uint32_t)n) a.ins_sorted[rb_wg + atomicAdd(bcur + gap / kBW, 1u)] = ev;
   }
@@ -1671,7 +1691,7 @@ struct mpc_plan {
   size_t ws_bytes = 0;
   uint8_t* ws = nullptr;
   std::vector<int32_t> work_parse, work_bc;  // int4 records
-  int n_parse_wg = 0, parse_lds = 0, nbmax = 1;
+  int n_parse_wg = 0, parse_lds = 0, nbmax = 1, parse_win = 1024, parse_nw = 8;
   int64_t n_bc = 0, units_cap = 0;
   int32_t shard = 0, n_shards = 1;
   bool fused = false;
@@ -1725,7 +1745,7 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.n_of = d.n_of; a.gbase = d.gbase;
   a.work = reinterpret_cast<const int4*>(p->ws + p->off[mpc_plan::B_WPARSE]);
   a.cs_base = d.cs_base; a.ovf_cap = d.ovf_cap; a.read_offset = d.read_offset; a.n_reads = d.N;
-  a.fused = p->fused ? 1 : 0; a.nbs = p->nbmax;
+  a.nbs = p->nbmax;
   a.i_end = d.i_end;
   a.ins_raw = at<uint64_t>(p, mpc_plan::B_INSRAW); a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
@@ -1735,11 +1755,20 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   return a;
 }
 
+static const void* parse_kernel(bool fused, int win) {
+  if (win == 512) return fused ? (const void*)K_parse<true, 512> : (const void*)K_parse<false, 512>;
+  return fused ? (const void*)K_parse<true, 1024> : (const void*)K_parse<false, 1024>;
+}
 static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
-  if (p->fused)
-    hipLaunchKernelGGL(K_parse<true>, dim3(p->n_parse_wg), dim3(kPW * 64), p->parse_lds, st, parse_args(p, d));
-  else
-    hipLaunchKernelGGL(K_parse<false>, dim3(p->n_parse_wg), dim3(kPW * 64), p->parse_lds, st, parse_args(p, d));
+  const dim3 g(p->n_parse_wg), b(p->parse_nw * 64);
+  const ParseArgs a = parse_args(p, d);
+  if (p->parse_win == 512) {
+    if (p->fused) hipLaunchKernelGGL((K_parse<true, 512>), g, b, p->parse_lds, st, a);
+    else hipLaunchKernelGGL((K_parse<false, 512>), g, b, p->parse_lds, st, a);
+  } else {
+    if (p->fused) hipLaunchKernelGGL((K_parse<true, 1024>), g, b, p->parse_lds, st, a);
+    else hipLaunchKernelGGL((K_parse<false, 1024>), g, b, p->parse_lds, st, a);
+  }
 }
 
 static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
@@ -1877,12 +1906,35 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       n_max = std::max<int64_t>(n_max, p->ref_len[s]);
       p->nbmax = std::max<int>(p->nbmax, (int)((p->ref_len[s] + 1 + kBW - 1) / kBW));
     }
+    // parse geometry: window size and waves per workgroup that give the most
+    // resident waves per CU with the position tallies in LDS (12 B per position)
     const int lds_cap = 160 * 1024;
-    p->fused = parse_lds_bytes((int)n_max, true, p->nbmax) <= lds_cap;
-    p->parse_lds = parse_lds_bytes((int)n_max, p->fused, p->nbmax);
-    if (p->parse_lds > lds_cap) { delete p; return fail(MPC_E_ARG, "reference too long for the LDS budget"); }
-    const int per_cu = std::max(1, std::min(4, lds_cap / p->parse_lds));
-    const int64_t target = 256 * std::min(per_cu, 2);
+    const int max_waves_cu = 16;  // VGPR budget of K_parse (~106 VGPRs -> 4 waves per SIMD)
+    auto lds_of = [&](int win, bool fu, int nw) {
+      return win == 512 ? parse_lds_bytes<512>((int)n_max, fu, p->nbmax, nw)
+                        : parse_lds_bytes<1024>((int)n_max, fu, p->nbmax, nw);
+    };
+    int best = -1, per_cu = 1;
+    for (int fu = 1; fu >= 0 && best < 0; --fu)
+      for (int win : {1024, 512})
+        for (int nw : {16, 12, 8}) {
+          const int lds = lds_of(win, fu != 0, nw);
+          if (lds > lds_cap) continue;
+          const int wgs = std::max(1, std::min(lds_cap / lds, max_waves_cu / nw));
+          const int waves = wgs * nw;
+          if (waves > best) { best = waves; p->fused = fu != 0; p->parse_win = win; p->parse_nw = nw; per_cu = wgs; }
+        }
+    if (best < 0) { delete p; return fail(MPC_E_ARG, "reference too long for the LDS budget"); }
+    p->parse_lds = lds_of(p->parse_win, p->fused, p->parse_nw);
+    if (const char* e = getenv("MPC_PARSE_GEOM")) {  // experiments: "win,nw"
+      int wv = 0, nv = 0;
+      if (sscanf(e, "%d,%d", &wv, &nv) == 2 && (wv == 512 || wv == 1024) && nv >= 1 && nv <= kMaxPW &&
+          lds_of(wv, p->fused, nv) <= lds_cap) {
+        p->parse_win = wv; p->parse_nw = nv; p->parse_lds = lds_of(wv, p->fused, nv);
+        per_cu = std::max(1, std::min(lds_cap / p->parse_lds, 32 / nv));
+      }
+    }
+    const int64_t target = 256 * per_cu;
     std::vector<int> pw_begin(p->S + 1, 0);
     for (int s = 0; s < p->S; ++s) {
       pw_begin[s] = (int)(p->work_parse.size() / 4);
@@ -1890,7 +1942,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       if (ns <= 0) continue;
       int64_t ch = std::max<int64_t>(1, (target * ns + std::max<int64_t>(p->N, 1) - 1) / std::max<int64_t>(p->N, 1));
       ch = std::min<int64_t>(ch, (ns + 63) / 64);
-      ch = std::max<int64_t>(ch, (ns + 65534) / 65535);  // LDS substitution tallies are 16-bit
+      ch = std::max<int64_t>(ch, (ns + 32766) / 32767);  // LDS tallies are 16-bit (<= 2 per read and position)
       for (int64_t c = 0; c < ch; ++c) {
         const int64_t x = a + ns * c / ch, y = a + ns * (c + 1) / ch;
         if (y > x) p->work_parse.insert(p->work_parse.end(), {s, (int32_t)x, (int32_t)y, 0});
@@ -2002,8 +2054,7 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WPARSE), p->work_parse.data(), 4 * p->work_parse.size(), hipMemcpyHostToDevice));
   if (!p->work_bc.empty())
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WBC), p->work_bc.data(), 4 * p->work_bc.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipFuncSetAttribute((const void*)K_parse<true>, hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
-  HIPCHK(hipFuncSetAttribute((const void*)K_parse<false>, hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
+  HIPCHK(hipFuncSetAttribute(parse_kernel(p->fused, p->parse_win), hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
   p->bound = true;
   return MPC_OK;
 }

@@ -1397,45 +1397,37 @@ __device__ __forceinline__ int code_exact(uint32_t c) {
   return c == expect ? code : -1;
 }
 
-constexpr int kStageB = 8192;  // flank bytes staged in LDS per side (the rest is read from HBM directly)
+constexpr int kStageB = 8192;  // flank bytes staged in LDS per chunk (a block's range is processed in chunks)
 
+// Byte-parallel: the block's flank bytes (both sides) are staged in LDS chunk by
+// chunk; every thread takes 4 consecutive bytes.  The owner of a byte is found
+// without a search: the starts of the block's non-empty flanks are bits of a
+// chunk bitmap with per-word prefix counts, so owner(x) = (starts <= x) - 1 in
+// the compacted list of non-empty flanks {start, row of byte 0}.
 __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
   __shared__ uint32_t win[2][kWinRows * 4];
-  __shared__ __attribute__((aligned(16))) uint8_t stage[2][kStageB + 16];
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kStageB + 16];
+  __shared__ int32_t t_start[kFR], t_row[kFR], t_read[kFR];  // compacted non-empty flanks of the current side
+  __shared__ uint32_t bm[kStageB / 32];                      // flank starts in the chunk
+  __shared__ int32_t wpre[kStageB / 32];                     // starts before each bitmap word (+ chunk base)
   __shared__ int32_t s_gap[2][kFR];
   __shared__ int64_t s_w0[2];
+  __shared__ int32_t s_w[4], s_nne, s_cbase;
   if (a.status[MPC_ST_FLAGS] & (DE_CAP | DE_INTERNAL)) return;
-  const int tid = threadIdx.x;
+  const int tid = threadIdx.x, l = lane(), w = tid >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * kFR;
   const int64_t r1 = r0 + kFR < a.N ? r0 + kFR : a.N;
   const int nr = (int)(r1 - r0);
   const int64_t tot = a.status[MPC_ST_ROWS_NEEDED];
   const int64_t r = r0 + tid;
   const bool live = tid < nr;
-  // level 1: per-read records and the block's byte ranges (independent loads)
+  // per-read records: flank byte ranges and the row of byte 0 of each flank
   int s = 0, ts = 0, ie = 0;
   int64_t off[2] = {0, 0}, end[2] = {0, 0};
   if (live) {
     s = a.sample[r]; ts = a.tstart[r]; ie = a.i_end[r];
     off[0] = a.up_off[r]; end[0] = a.up_off[r + 1];
     off[1] = a.down_off[r]; end[1] = a.down_off[r + 1];
-  }
-  const int64_t B0[2] = {a.up_off[r0], a.down_off[r0]};
-  const int64_t B1[2] = {a.up_off[r1], a.down_off[r1]};
-  // level 2: stage the block's flank bytes (16 B per lane, coalesced) while the layout loads fly
-  int64_t A0[2];
-#pragma unroll
-  for (int side = 0; side < 2; ++side) {
-    const uint8_t* src = side ? a.down : a.up;
-    A0[side] = B0[side] & ~(int64_t)15;
-    const int64_t nb = B1[side] - A0[side];
-    const int64_t nst = nb < kStageB ? nb : kStageB;
-#ifdef MPC_EXP_NOSTAGE_FLANK
-    for (int64_t x = 16 * tid; x < 0; x += 16 * blockDim.x)
-#else
-    for (int64_t x = 16 * tid; x < nst; x += 16 * blockDim.x)
-#endif
-      *reinterpret_cast<uint4*>(&stage[side][x]) = *reinterpret_cast<const uint4*>(src + A0[side] + x);
   }
   for (int k = tid; k < 2 * kWinRows * 4; k += blockDim.x) (&win[0][0])[k] = 0;
   int64_t rs[2] = {-1, -1};
@@ -1472,67 +1464,122 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
     const int32_t gw = (x == y || x == z) ? x : y;
     s_w0[tid] = gw >= 0 ? (int64_t)a.row_base[gw] : (int64_t)INT32_MIN;
   }
-  __syncthreads();
   uint32_t lerr = 0;
+  int64_t lread = INT64_MAX;
 #pragma unroll 1
-#ifdef MPC_EXP_NOLOOP_FLANK
-  for (int side = 0; side < 0; ++side) {
-#else
   for (int side = 0; side < 2; ++side) {
-#endif
+    const uint8_t* src = side ? a.down : a.up;
+    const int64_t B0 = side ? a.down_off[r0] : a.up_off[r0];
+    const int64_t nb = (side ? a.down_off[r1] : a.up_off[r1]) - B0;  // bytes of the block's flanks
+    // compacted list of non-empty flanks (in read order: starts strictly increase)
+    const int64_t L = end[side] - off[side];
+    const bool ne = live && L > 0;
+    if (ne && (rs[side] >= 0) && rs[side] + L > tot) lerr |= DE_INTERNAL;
+    const int f = ne ? 1 : 0;
+    const int inc = wave_scan_i32(f);
+    __syncthreads();  // previous side / window vote done with the shared tables
+    if (l == 63) s_w[w] = inc;
+    __syncthreads();
+    int wp = 0;
+    for (int k = 0; k < w; ++k) wp += s_w[k];
+    const int c = wp + inc - f;
+    if (ne) {
+      t_start[c] = (int32_t)(off[side] - B0);
+      t_row[c] = (rs[side] >= 0 && rs[side] + L <= tot) ? (int32_t)rs[side] : -1;
+      t_read[c] = tid;
+    }
+    if (tid == 255) s_nne = wp + inc;
     const int64_t w0 = s_w0[side];
     uint32_t* wn = win[side];
-    const int64_t o = off[side];
-    const int64_t rsg = rs[side];
-    const int64_t Lg = rsg >= 0 ? end[side] - o : 0;
-    if (Lg > 0 && rsg + Lg > tot) lerr |= DE_INTERNAL;
-    const int L = (Lg > 0 && rsg + Lg <= tot) ? (int)(Lg > (1 << 30) ? (1 << 30) : Lg) : 0;
-    // staged bytes come from LDS, the rest (a very long block range) from HBM; generic pointer
-    const int64_t rel = o - A0[side];
-#ifdef MPC_EXP_NOSTAGE_FLANK
-    const bool staged = false;
-#else
-    const bool staged = rel + L <= kStageB;
+    for (int64_t c0 = 0; c0 < nb; c0 += kStageB) {  // chunks of the block's byte range
+      const int64_t cn = nb - c0 < kStageB ? nb - c0 : kStageB;
+      __syncthreads();
+      // stage [B0 + c0, B0 + c0 + cn) at stage[(B0 + c0) & 15 ...]
+      const int64_t A0 = (B0 + c0) & ~(int64_t)15;
+      const int sh0 = (int)((B0 + c0) - A0);
+#ifndef MPC_EXP_NOSTAGE_FLANK
+      for (int64_t x = 16 * tid; x < sh0 + cn; x += 16 * blockDim.x)
+        *reinterpret_cast<uint4*>(&stage[x]) = *reinterpret_cast<const uint4*>(src + A0 + x);
 #endif
-    const uint8_t* src = staged ? &stage[side][0] + rel : (side ? a.down : a.up) + o;
-    const uint8_t* base = reinterpret_cast<const uint8_t*>((uintptr_t)src & ~(uintptr_t)3);
-    const uint32_t sh = (uint32_t)((uintptr_t)src & 3);
-    const int64_t rw = rsg - w0;  // window row of byte 0
-    // chunks of 4 bytes in a per-lane rotated order: lanes of a wave hit different
-    // rows (every downstream flank starts at the same row, LDS atomics would collide)
-    const int nch = (L + 3) >> 2;
-    int c = nch > 0 ? (int)(lane() % nch) : 0;
-    for (int it = 0; it < nch; ++it, c = (c + 1 == nch) ? 0 : c + 1) {
-      const int j = 4 * c;
-      const uint32_t v = __builtin_amdgcn_alignbyte(*reinterpret_cast<const uint32_t*>(base + j + 4),
-                                                    *reinterpret_cast<const uint32_t*>(base + j), sh);
+      for (int k = tid; k < kStageB / 32; k += blockDim.x) bm[k] = 0;
+      if (tid == 0) {  // owner of the chunk's first byte: last non-empty flank starting <= c0
+        int lo = 0, hi = s_nne - 1;
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (t_start[mid] <= c0) lo = mid; else hi = mid - 1;
+        }
+        s_cbase = lo;
+      }
+      __syncthreads();
+      if (ne) {
+        const int64_t rel = (off[side] - B0) - c0;
+        if (rel > 0 && rel < cn) atomicOr(&bm[rel >> 5], 1u << (rel & 31));
+      }
+      __syncthreads();
+      {  // per-word prefix of the start bits (block scan, one word per thread)
+        const int nwd = (int)((cn + 31) >> 5);
+        const int cnt = tid < nwd ? __popc(bm[tid]) : 0;
+        const int i2 = wave_scan_i32(cnt);
+        if (l == 63) s_w[w] = i2;
+        __syncthreads();
+        int p2 = s_cbase;
+        for (int k = 0; k < w; ++k) p2 += s_w[k];
+        if (tid < nwd) wpre[tid] = p2 + i2 - cnt;
+      }
+      __syncthreads();
+#ifdef MPC_EXP_NOBYTES_FLANK
+      for (int x0 = 4 * tid; x0 < 0; x0 += 4 * blockDim.x) {
+#else
+      for (int x0 = 4 * tid; x0 < cn; x0 += 4 * blockDim.x) {
+#endif
+        const uint32_t* b32 = reinterpret_cast<const uint32_t*>(stage);
+        const int sx = x0 + sh0;
+        const uint32_t v = __builtin_amdgcn_alignbyte(b32[(sx >> 2) + 1], b32[sx >> 2], (uint32_t)(sx & 3));
+        const uint32_t word = bm[x0 >> 5];
+        const int bpos = x0 & 31;
+        int cur = wpre[x0 >> 5] + __popc(word & ((bpos == 0) ? 0u : ((1u << bpos) - 1u)));  // starts before x0
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int jj = j + k;
-        if (jj >= L) break;
-        const int code = code_exact((v >> (8 * k)) & 0xffu);
-        if (code < 0) { lerr |= DE_KEY; continue; }  // flank base not in the dict (:61, :71)
-        const int64_t wr = rw + jj;
-        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 4 + code, 1u);
-        else atomicAdd(a.rows + (rsg + jj) * 4 + code, 1u);
+        for (int k = 0; k < 4; ++k) {
+          const int x = x0 + k;
+          if (x >= cn) break;
+          cur += (word >> (bpos + k)) & 1u;
+          const int o = cur;  // owner: index in the compacted list
+          const int32_t rw = t_row[o];
+          if (rw < 0) continue;
+          const int64_t row = (int64_t)rw + (c0 + x - t_start[o]);
+          const int code = code_exact((v >> (8 * k)) & 0xffu);
+          if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
+          const int64_t wr = row - w0;
+#ifdef MPC_EXP_NOATOM_FLANK
+          lread ^= (wr + code);
+          if (true) {} else
+#endif
+          if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 4 + code, 1u);
+          else {
+            atomicAdd(a.rows + row * 4 + code, 1u);
+#ifdef MPC_EXP_COUNT_FLANK
+            atomicAdd(&a.status[6], 1u);
+#endif
+          }
+        }
       }
     }
   }
   __syncthreads();
-#ifdef MPC_EXP_NOFLUSH_FLANK
-  for (int side = 0; side < 0; ++side) {
-#else
   for (int side = 0; side < 2; ++side) {
-#endif
     const int64_t w0 = s_w0[side];
     for (int k = tid; k < kWinRows * 4; k += blockDim.x) {
       const uint32_t v = win[side][k];
       if (v) atomicAdd(a.rows + w0 * 4 + k, v);
     }
   }
+#ifdef MPC_EXP_NOATOM_FLANK
+  if (lread == 12345) a.status[7] = 1;
+  lread = INT64_MAX;
+#endif
   if (lerr) {
     atomicOr(&a.status[MPC_ST_FLAGS], lerr);
-    if (lerr & DE_KEY) atomicMin(&a.status[MPC_ST_FIRST_READ], (uint32_t)r);
+    if (lread != INT64_MAX) atomicMin(&a.status[MPC_ST_FIRST_READ], (uint32_t)lread);
   }
 }
 

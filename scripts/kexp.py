@@ -35,6 +35,8 @@ if hasattr(L, "mpc_prof_parse"):
     L.mpc_prof_parse(buf, 1)
     v = list(buf)[:8]
     out["prof"] = dict(zip(["stage", "toklist", "rounds", "carry", "windows", "rounds_n", "total"], v[:7]))
+st = r.plan.status()
+out["status"] = [int(x) for x in st]
 t0 = time.perf_counter()
 for _ in range(20): r.step(0.1, 5.0)
 torch.cuda.synchronize()

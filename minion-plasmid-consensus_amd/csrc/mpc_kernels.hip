@@ -157,7 +157,7 @@ struct alignas(16) WaveLds {            // per-wave LDS of K_parse
   uint8_t stage[WIN + 16];              // window bytes (+16: word reads past the end)
   uint8_t em[WIN / 8];                  // boundary bits (special characters | read starts), bit = byte
   uint8_t ra[WIN / 8];                  // read-start bits
-  uint16_t tok[WIN + 2];                // token starts in [P, C), then the sentinel C; bit 15 = read start
+  uint16_t tok[WIN + 2 + 64];           // token starts in [P, C), then the sentinel C; bit 15 = read start (+64: unconditional loads)
 };
 
 struct ParseArgs {  // slim argument block (no SGPR spills)
@@ -798,16 +798,14 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
     kb[(passes + 1) & 1] = d.keys_tmp; vb[(passes + 1) & 1] = d.vals_tmp;
   }
   __syncthreads();
-  // gather (read order) into buffer 0
-  for (int64_t i = tid; i < M; i += kRS) {
-    int lo = 0, hi = nblocks - 1;  // last block with bpre <= i
-    while (lo < hi) {
-      const int mid = (lo + hi + 1) >> 1;
-      if (d.bpre[mid] <= i) lo = mid; else hi = mid - 1;
+  // gather (read order) into buffer 0: one source block per thread (short, independent copies)
+  for (int b = tid; b < nblocks; b += kRS) {
+    const int c = d.bcnt[b];
+    const int o = d.bpre[b];
+    for (int j = 0; j < c; ++j) {
+      kb[0][o + j] = d.keys_in[(int64_t)b * kRS + j];
+      vb[0][o + j] = d.vals_in[(int64_t)b * kRS + j];
     }
-    const int64_t src = (int64_t)lo * kRS + (i - d.bpre[lo]);
-    kb[0][i] = d.keys_in[src];
-    vb[0][i] = d.vals_in[src];
   }
   __syncthreads();
   const uint64_t lt = (1ull << l) - 1ull;
@@ -1595,69 +1593,117 @@ __device__ __forceinline__ int sample_of_row(const Dev& d, int64_t row) {
   return lo;
 }
 
+// first row of every sample in LDS (kSmpLds samples; beyond that the global search)
+constexpr int kSmpLds = 512;
+__device__ __forceinline__ void load_sample_rows(const Dev& d, int32_t* srow) {
+  for (int s = threadIdx.x; s < d.S && s < kSmpLds; s += blockDim.x) srow[s] = d.row_base[d.gbase[s]];
+}
+__device__ __forceinline__ int sample_of_row_lds(const Dev& d, const int32_t* srow, int64_t row) {
+  if (d.S > kSmpLds) return sample_of_row(d, row);
+  int lo = 0, hi = d.S - 1;
+  while (lo < hi) {
+    const int mid = (lo + hi + 1) >> 1;
+    if (srow[mid] <= row) lo = mid; else hi = mid - 1;
+  }
+  return lo;
+}
+
+constexpr int kCB = 1024;  // rows per block of the consensus kernels (4 per thread)
+
+// per slot: sorted(tuples in dict order, key=count)[::-1] -> top / second / tie -> N (:363-423)
+__device__ __forceinline__ uint4 call_slot(uint4 cv, double gtf, uint32_t* total_out) {
+  const uint32_t c[4] = {cv.x, cv.y, cv.z, cv.w};  // A, T, C, G
+  const uint32_t total = c[0] + c[1] + c[2] + c[3];
+  *total_out = total;
+  if (total == 0) return make_uint4(0, 0, 0, 0);
+  // descending count, ties in reverse dict order (stable sort then reverse, :371-374)
+  int idx[4], m = 0;
+  for (int k = 3; k >= 0; --k) if (c[k] > 0) idx[m++] = k;   // reverse dict order
+  for (int a = 1; a < m; ++a) {                               // stable sort descending
+    const int t = idx[a];
+    int b = a - 1;
+    while (b >= 0 && c[idx[b]] < c[t]) { idx[b + 1] = idx[b]; --b; }
+    idx[b + 1] = t;
+  }
+  const char names[4] = {'A', 'T', 'C', 'G'};
+  uint32_t base, base2, count, count2;
+  if (m == 1 || c[idx[0]] > c[idx[1]]) { base = names[idx[0]]; count = c[idx[0]]; }
+  else { base = 'N'; count = 0; for (int a = 0; a < m; ++a) if (c[idx[a]] == c[idx[0]]) count += c[idx[a]]; }
+  if (m <= 1) { base2 = 'X'; count2 = 0; }
+  else if (m == 2 || c[idx[1]] > c[idx[2]]) { base2 = names[idx[1]]; count2 = c[idx[1]]; }
+  else { base2 = 'N'; count2 = 0; for (int a = 0; a < m; ++a) if (c[idx[a]] == c[idx[1]]) count2 += c[idx[a]]; }
+  const uint32_t chrom1 = base;
+  if ((double)count < gtf * (double)count2) base = 'N';   // :421
+  return make_uint4(base | (chrom1 << 8) | (base2 << 16) | (1u << 24), count, count2, total);
+}
+
+// calls of every row + max depth over slot 0 (:332-341); rows t + 256 k of the block
 __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
-  __shared__ int64_t s_key;
-  __shared__ int32_t s_val;
+  __shared__ int32_t srow[kSmpLds];
+  __shared__ int32_t s_blk[2], s_w[4];
   const bool cap = (d.status[MPC_ST_FLAGS] & DE_CAP) != 0;
-  const int64_t need = cap ? 0 : (int64_t)d.status[MPC_ST_ROWS_NEEDED];
-  for (int64_t row0 = (int64_t)blockIdx.x * blockDim.x; row0 < R; row0 += (int64_t)gridDim.x * blockDim.x) {
-    const int64_t row = row0 + threadIdx.x;
-    uint4 out = make_uint4(0, 0, 0, 0);
-    uint32_t slot0 = 0;
-    int smp = -1;
-    if (row < R && row < need) {
-      const uint4 cv = reinterpret_cast<const uint4*>(d.rows)[row];
-      const uint32_t c[4] = {cv.x, cv.y, cv.z, cv.w};  // A, T, C, G
-      const uint8_t mt = d.meta[row];
-      const uint32_t total = c[0] + c[1] + c[2] + c[3];
-      if (total > 0) {
-        // sorted(tuples in dict order, key=count)[::-1]: descending count, ties in
-        // reverse dict order (stable sort then reverse, :371-374)
-        int idx[4], m = 0;
-        for (int k = 3; k >= 0; --k) if (c[k] > 0) idx[m++] = k;   // reverse dict order
-        for (int a = 1; a < m; ++a) {                               // stable sort descending
-          const int t = idx[a];
-          int b = a - 1;
-          while (b >= 0 && c[idx[b]] < c[t]) { idx[b + 1] = idx[b]; --b; }
-          idx[b + 1] = t;
-        }
-        const char names[4] = {'A', 'T', 'C', 'G'};
-        uint32_t base, base2, count, count2;
-        if (m == 1 || c[idx[0]] > c[idx[1]]) { base = names[idx[0]]; count = c[idx[0]]; }
-        else { base = 'N'; count = 0; for (int a = 0; a < m; ++a) if (c[idx[a]] == c[idx[0]]) count += c[idx[a]]; }
-        if (m <= 1) { base2 = 'X'; count2 = 0; }
-        else if (m == 2 || c[idx[1]] > c[idx[2]]) { base2 = names[idx[1]]; count2 = c[idx[1]]; }
-        else { base2 = 'N'; count2 = 0; for (int a = 0; a < m; ++a) if (c[idx[a]] == c[idx[1]]) count2 += c[idx[a]]; }
-        const uint32_t chrom1 = base;
-        if ((double)count < d.gtf * (double)count2) base = 'N';   // :421
-        out = make_uint4(base | (chrom1 << 8) | (base2 << 16) | (1u << 24), count, count2, total);
-        if (mt & 2u) { slot0 = total; smp = sample_of_row(d, row); }  // slot 0 only (:336)
-      }
-    }
+  const int64_t need0 = cap ? 0 : (int64_t)d.status[MPC_ST_ROWS_NEEDED];
+  const int64_t need = need0 < R ? need0 : R;
+  load_sample_rows(d, srow);
+  const int64_t b0 = (int64_t)blockIdx.x * kCB;
+  __syncthreads();
+  if (threadIdx.x < 2) {
+    const int64_t rr = threadIdx.x == 0 ? b0 : (b0 + kCB < need ? b0 + kCB : need) - 1;
+    s_blk[threadIdx.x] = rr >= 0 ? sample_of_row_lds(d, srow, rr) : 0;
+  }
+  uint4 cv[4];
+  uint8_t mt[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {  // all loads first
+    const int64_t row = b0 + threadIdx.x + 256 * k;
+    cv[k] = row < need ? reinterpret_cast<const uint4*>(d.rows)[row] : make_uint4(0, 0, 0, 0);
+    mt[k] = row < need ? d.meta[row] : 0;
+  }
+  __syncthreads();
+  const bool one = s_blk[0] == s_blk[1];
+  int32_t mx = -1;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int64_t row = b0 + threadIdx.x + 256 * k;
+    uint32_t total = 0;
+    const uint4 out = call_slot(cv[k], d.gtf, &total);
     if (row < R) reinterpret_cast<uint4*>(d.res)[row] = out;
-    // max depth: block-aggregated (same-address atomics serialize)
-    block_atomic_max(reinterpret_cast<int32_t*>(d.maxdepth), smp, (int32_t)slot0, smp >= 0, &s_key, &s_val);
+    if (total > 0 && (mt[k] & 2u)) {  // slot 0 only (:336)
+      if (one) mx = (int32_t)total > mx ? (int32_t)total : mx;
+      else atomicMax(d.maxdepth + sample_of_row_lds(d, srow, row), total);
+    }
+  }
+  if (one) {  // the block's rows are one sample: one atomic per block
+    mx = wave_max(mx);
+    if (lane() == 0) s_w[threadIdx.x >> 6] = mx;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int32_t m = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
+      if (m >= 0) atomicMax(d.maxdepth + s_blk[0], (uint32_t)m);
+    }
   }
 }
 
 // keep[row] = emitted (:428) and per-block counts (kKB rows per block)
-constexpr int kKB = 1024;
-__device__ __forceinline__ bool keep_row(const Dev& d, int64_t row, uint4 v) {
-  if (!(v.x >> 24)) return false;
-  const int s = sample_of_row(d, row);
-  const double thr = (double)d.maxdepth[s] * d.mdf;  // :338
-  return (double)v.y > thr;                           // :428
-}
-
+constexpr int kKB = kCB;
 __global__ __launch_bounds__(256) void K_keep(Dev d, int64_t R) {
+  __shared__ int32_t srow[kSmpLds];
   __shared__ int32_t s_w[4];
+  load_sample_rows(d, srow);
   const int64_t base = (int64_t)blockIdx.x * kKB + 4 * threadIdx.x;
+  uint4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = base + k < R ? reinterpret_cast<const uint4*>(d.res)[base + k] : make_uint4(0, 0, 0, 0);
+  __syncthreads();
   int c = 0;
   uint32_t bits = 0;
 #pragma unroll
   for (int k = 0; k < 4; ++k) {
-    const int64_t row = base + k;
-    if (row < R && keep_row(d, row, reinterpret_cast<const uint4*>(d.res)[row])) { ++c; bits |= 1u << k; }
+    if (v[k].x >> 24) {
+      const int s = sample_of_row_lds(d, srow, base + k);
+      const double thr = (double)d.maxdepth[s] * d.mdf;  // :338
+      if ((double)v[k].y > thr) { ++c; bits |= 1u << k; }  // :428
+    }
   }
   d.keep[(int64_t)blockIdx.x * 256 + threadIdx.x] = (int32_t)bits;
   c = wave_sum(c);
@@ -1709,6 +1755,7 @@ __global__ __launch_bounds__(256) void K_emit(Dev d, int64_t R) {
       for (int k = 0; k < (int)((rb - b0) & 3); ++k) q += (bits >> k) & 1u;
       d.ncalls[s] = (int32_t)q;
     }
+    if (blockIdx.x == 0 && threadIdx.x == 0 && rb >= nb * kKB) d.ncalls[s] = (int32_t)all;
   }
   if (blockIdx.x == 0 && threadIdx.x == 0) d.ncalls[d.S] = (int32_t)all;
 }
@@ -2225,7 +2272,7 @@ int mpc_consensus(mpc_plan* p, double mdf, double gtf, void* stream) {
   d.mdf = mdf;
   d.gtf = gtf;
   const int64_t R = p->row_cap;
-  hipLaunchKernelGGL(K_call, dim3(nblk(R)), dim3(256), 0, st, d, R);
+  hipLaunchKernelGGL(K_call, dim3(nblk(R, kCB)), dim3(256), 0, st, d, R);
   hipLaunchKernelGGL(K_keep, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R);
   hipLaunchKernelGGL(K_emit, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R);
   HIPCHK(hipGetLastError());

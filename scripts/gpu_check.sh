@@ -11,4 +11,4 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 5 "$@" > gpurun_out/b.log 
 grep metric gpurun_out/b.log
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $R/gpurun_out/prof -o run --output-format csv -- python3 $R/bench.py --steps 20 --warmup 5 --no-cpu-baseline > $R/gpurun_out/p.log 2>&1 || { tail -20 $R/gpurun_out/p.log; exit 1; }
-python3 $R/scripts/kstats.py $R/gpurun_out/prof | head -12
+python3 $R/scripts/kstats.py $R/gpurun_out/prof 14

@@ -65,10 +65,17 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    # one rank per GPU; the modulo only matters for rehearsals with more ranks than GPUs
+    local = local % max(1, torch.cuda.device_count())
     torch.cuda.set_device(local)
+    # RCCL ("nccl") over xGMI; MPC_DIST_BACKEND=gloo rehearses the N>1 path on one GPU
+    backend = os.environ.get("MPC_DIST_BACKEND", "nccl")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
     pkg = importlib.import_module("minion-plasmid-consensus_amd")
     eng = pkg.engine
 
@@ -82,7 +89,12 @@ def main():
     else:
         runner = eng.Runner(samples, device=local)
     batch = runner.batch
-    aligned = batch.aligned_bases * world  # weak scaling: every rank holds an equal shard
+    aligned = batch.aligned_bases  # weak scaling: every rank holds a C2-sized shard of one pileup
+    coll_dev = "cuda" if backend == "nccl" else "cpu"
+    if world > 1:
+        t = torch.tensor([aligned], dtype=torch.int64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        aligned = int(t.item())
 
     mdf, gtf = 0.1, 5.0  # config.yaml:38-39 (MIN_BASE_FACTOR, GLOBAL_THRESHOLD_FACTOR)
     for _ in range(max(1, args.warmup)):
@@ -103,7 +115,7 @@ def main():
     barrier()
     dt = time.perf_counter() - t0
     if world > 1:
-        t = torch.tensor([dt], dtype=torch.float64, device="cuda")
+        t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms = dt * 1e3 / args.steps

@@ -1,0 +1,63 @@
+/*
+ * mpc_ingest.h -- C-ABI of libmpc_ingest.so: native host ingest (Steps 1-3 of
+ * /root/reference/src/mapped_paf_read_parser.py) for the drop-in CLI.
+ *
+ *   reference                                     replaced by
+ *   --------------------------------------------  ----------------------------------
+ *   Step 1 reference FASTA          :161-184      mpc_ingest(): ref
+ *   Step 2 PAF, first alignment per read :192-245 mpc_ingest(): cs, tstart, qs/qe flip
+ *   Step 3 reads FASTA, revcomp, flanks :253-277  mpc_ingest(): up, down
+ *
+ * Same results as minion-plasmid-consensus_amd/ingest.py (the Python
+ * restatement of those steps): memory-mapped files, multi-threaded line
+ * parsing, first-occurrence dedup of PAF records, last-wins for duplicate
+ * FASTA names, Python slicing for the flanks.
+ *
+ * status
+ *   MPC_INGEST_OK        outputs valid
+ *   MPC_INGEST_ERROR     the reference raises on this input (exit 1); message says why
+ *   MPC_INGEST_FALLBACK  an input feature this parser does not restate (non-ASCII bytes,
+ *                        '\r' line ends, integers Python accepts that are not plain digits):
+ *                        the caller uses the Python ingest, which has the exact semantics
+ * Outputs are owned by the library: release them with mpc_ingest_free().
+ */
+#ifndef MPC_INGEST_H
+#define MPC_INGEST_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MPC_INGEST_OK 0
+#define MPC_INGEST_ERROR 1
+#define MPC_INGEST_FALLBACK 2
+
+typedef struct {
+  uint8_t* ref;         /* concatenated, rstrip()ed, upper-cased reference (:163-165) */
+  int64_t ref_len;
+  uint8_t* cs;          /* cs tags after "cs:" (:231-234), retained reads in PAF first-occurrence order */
+  int64_t* cs_off;      /* [n_reads + 1] */
+  int64_t* tstart;      /* [n_reads] PAF column 8 (:222) */
+  uint8_t* up;          /* upstream flanks seq[:qs'] (:264) */
+  int64_t* up_off;      /* [n_reads + 1] */
+  uint8_t* down;        /* downstream flanks seq[qe':] (:265) */
+  int64_t* down_off;    /* [n_reads + 1] */
+  int64_t* aligned;     /* [n_reads] qe' - qs' (aligned bases) */
+  int64_t n_reads;      /* retained reads (first alignment per name, :237-243) */
+  int64_t n_alignments; /* PAF lines (:213) */
+  int32_t status;       /* MPC_INGEST_* */
+  char message[256];
+} mpc_ingest_out;
+
+int mpc_ingest_version(void);
+/* n_threads <= 0: all hardware threads.  Returns out->status. */
+int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_path, int n_threads,
+               mpc_ingest_out* out);
+void mpc_ingest_free(mpc_ingest_out* out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MPC_INGEST_H */

@@ -3,6 +3,7 @@ the repo snapshot to the GPU box).
 
   libmpc.so        HIP kernels + C-ABI (include/mpc.h), hipcc --offload-arch=gfx950
   libmpc_synth.so  host-only synthetic data generator (g++)
+  libmpc_ingest.so native host ingest, Steps 1-3 (include/mpc_ingest.h, g++ -pthread)
 """
 import os
 import subprocess
@@ -13,6 +14,7 @@ CSRC = os.path.join(PKG, "csrc")
 INCLUDE = os.path.join(REPO, "include")
 LIBMPC = os.path.join(PKG, "libmpc.so")
 LIBSYNTH = os.path.join(PKG, "libmpc_synth.so")
+LIBINGEST = os.path.join(PKG, "libmpc_ingest.so")
 
 HIP_SOURCES = ["mpc_kernels.hip"]
 HIP_HEADERS = ["mpc_device.h"]
@@ -36,6 +38,15 @@ def ensure_synth():
     return build_synth()
 
 
+def build_ingest(force=False):
+    src = os.path.join(CSRC, "ingest.cpp")
+    hdr = os.path.join(INCLUDE, "mpc_ingest.h")
+    if force or _stale(LIBINGEST, [src, hdr]):
+        subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-I", INCLUDE, "-o", LIBINGEST, src],
+                       check=True)
+    return LIBINGEST
+
+
 def build_hip(force=False, extra=()):
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [os.path.join(INCLUDE, "mpc.h")]
@@ -49,4 +60,5 @@ def build_hip(force=False, extra=()):
 
 def build_all(force=False):
     build_synth(force)
+    build_ingest(force)
     build_hip(force)

@@ -1,0 +1,382 @@
+// ingest.cpp -- native host ingest: Steps 1-3 of
+// /root/reference/src/mapped_paf_read_parser.py behind include/mpc_ingest.h.
+//
+// The result is byte-identical to minion-plasmid-consensus_amd/ingest.py (the
+// Python restatement the CLI falls back to):
+//   Step 1 (:161-184)  every non-'>' line of the reference, rstrip()ed and
+//                      upper-cased, concatenated
+//   Step 2 (:192-245)  per PAF line: rstrip().split('\t'); int() of columns 1, 2,
+//                      3, 7; minus strand flips (qs, qe) to (qlen-qe, qlen-qs);
+//                      cs = first field starting with "cs:", without "cs:";
+//                      the FIRST line of a read name wins
+//   Step 3 (:253-277)  per reads-FASTA record named in the PAF: sequence lines
+//                      rstrip()ed, upper-cased, joined; minus strand reverse-
+//                      complemented (KeyError outside ACGTN); upstream = seq[:qs],
+//                      downstream = seq[qe:] with Python slicing; a duplicate
+//                      name is processed again and the last record wins
+// Host-side only (g++ -pthread); the files are memory-mapped and parsed by
+// all cores: PAF lines and FASTA records are independent, only the PAF dedup
+// (file order) is sequential.
+#include "mpc_ingest.h"
+
+#include <fcntl.h>
+#include <sys/mman.h>
+#include <sys/stat.h>
+#include <unistd.h>
+
+#include <algorithm>
+#include <atomic>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <string_view>
+#include <thread>
+#include <unordered_map>
+#include <vector>
+
+namespace {
+
+using sv = std::string_view;
+
+struct Mapped {
+  const char* p = "";
+  size_t n = 0;
+  void* m = nullptr;
+  int fd = -1;
+  Mapped() = default;
+  Mapped(const Mapped&) = delete;
+  ~Mapped() {
+    if (m && m != MAP_FAILED) munmap(m, n);
+    if (fd >= 0) close(fd);
+  }
+  bool open(const char* path) {
+    fd = ::open(path, O_RDONLY);
+    if (fd < 0) return false;
+    struct stat st;
+    if (fstat(fd, &st) != 0) return false;
+    n = (size_t)st.st_size;
+    if (n == 0) return true;
+    m = mmap(nullptr, n, PROT_READ, MAP_PRIVATE, fd, 0);
+    if (m == MAP_FAILED) return false;
+    madvise(m, n, MADV_SEQUENTIAL);
+    p = static_cast<const char*>(m);
+    return true;
+  }
+};
+
+// str.isspace() restricted to ASCII (what rstrip() removes)
+inline bool py_space(unsigned char c) { return c == ' ' || (c >= 9 && c <= 13) || (c >= 0x1c && c <= 0x1f); }
+inline sv rstrip(sv s) {
+  size_t e = s.size();
+  while (e > 0 && py_space((unsigned char)s[e - 1])) --e;
+  return s.substr(0, e);
+}
+inline char upper(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 32) : c; }
+
+template <class F>
+void parallel(int T, F f) {
+  if (T <= 1) { f(0); return; }
+  std::vector<std::thread> th;
+  th.reserve(T);
+  for (int k = 0; k < T; ++k) th.emplace_back(f, k);
+  for (auto& t : th) t.join();
+}
+
+// bytes Python decodes or translates in text mode: anything >= 0x80, '\r'
+bool needs_python(const Mapped& f, int T) {
+  std::atomic<bool> bad{false};
+  parallel(T, [&](int k) {
+    const size_t a = f.n * k / T, b = f.n * (k + 1) / T;
+    for (size_t i = a; i < b && !bad.load(std::memory_order_relaxed);) {
+      const size_t e = std::min(b, i + (size_t)(1 << 16));
+      unsigned x = 0;
+      for (; i < e; ++i) {
+        const unsigned char c = (unsigned char)f.p[i];
+        x |= (unsigned)(c >= 0x80) | (unsigned)(c == '\r');
+      }
+      if (x) bad = true;
+    }
+  });
+  return bad.load();
+}
+
+// [a, b) moved forward to line starts (a line = up to and including '\n'; a last
+// line without '\n' counts)
+inline size_t line_start_at_or_after(const Mapped& f, size_t x) {
+  if (x == 0) return 0;
+  if (x >= f.n) return f.n;
+  const void* nl = memchr(f.p + x - 1, '\n', f.n - (x - 1));
+  return nl ? (size_t)(static_cast<const char*>(nl) - f.p) + 1 : f.n;
+}
+
+// Python int() of a plain decimal field: [-]digits.  0 = ok, 1 = not an int for
+// Python either (empty, stray chars), 2 = let Python decide (sign '+', spaces,
+// '_', very long)
+int plain_int(sv s, int64_t* out) {
+  if (s.empty()) return 1;
+  size_t i = 0;
+  bool neg = false;
+  if (s[0] == '-') { neg = true; i = 1; }
+  if (i >= s.size()) return 1;
+  if (s.size() - i > 18) return 2;
+  int64_t v = 0;
+  for (; i < s.size(); ++i) {
+    const char c = s[i];
+    if (c < '0' || c > '9') return (c == '+' || c == '_' || py_space((unsigned char)c)) ? 2 : 1;
+    v = v * 10 + (c - '0');
+  }
+  *out = neg ? -v : v;
+  return 0;
+}
+
+struct Fail {
+  int code = MPC_INGEST_OK;  // OK / ERROR / FALLBACK
+  size_t pos = SIZE_MAX;     // file position of the first failing line (errors are reported in file order)
+  std::string msg;
+  void set(int c, size_t p, std::string m) {
+    if (c == MPC_INGEST_FALLBACK) {
+      if (code != MPC_INGEST_FALLBACK) { code = c; pos = p; msg = std::move(m); }
+    } else if (code == MPC_INGEST_OK || (code == MPC_INGEST_ERROR && p < pos)) {
+      code = c; pos = p; msg = std::move(m);
+    }
+  }
+  void merge(const Fail& o) {
+    if (o.code != MPC_INGEST_OK) set(o.code, o.pos, o.msg);
+  }
+};
+
+struct PafRec {
+  sv name, cs;
+  int64_t qs, qe, ts;
+  bool minus;
+};
+
+// one PAF line (:197-234)
+int parse_paf_line(sv line, PafRec* r, std::string* err) {
+  const sv s = rstrip(line);
+  sv f[8];
+  int nf = 0;
+  sv cs;
+  bool have_cs = false;
+  size_t b = 0;
+  for (;;) {  // split('\t'): every field, the cs tag may be anywhere
+    const size_t e = s.find('\t', b);
+    const sv fld = s.substr(b, e == sv::npos ? sv::npos : e - b);
+    if (nf < 8) f[nf] = fld;
+    ++nf;
+    if (!have_cs && fld.size() >= 3 && fld.compare(0, 3, "cs:") == 0) { cs = fld.substr(3); have_cs = true; }
+    if (e == sv::npos) break;
+    b = e + 1;
+  }
+  int64_t qlen = 0, qs = 0, qe = 0, ts = 0;
+  const int idx[4] = {1, 2, 3, 7};
+  int64_t* dst[4] = {&qlen, &qs, &qe, &ts};
+  for (int k = 0; k < 4; ++k) {  // int(line[1]), int(line[2]), int(line[3]), int(line[7])
+    if (idx[k] >= nf) { *err = "IndexError: list index out of range"; return MPC_INGEST_ERROR; }
+    const int rc = plain_int(f[idx[k]], dst[k]);
+    if (rc == 2) return MPC_INGEST_FALLBACK;
+    if (rc == 1) { *err = "ValueError: invalid literal for int(): '" + std::string(f[idx[k]].substr(0, 40)) + "'"; return MPC_INGEST_ERROR; }
+  }
+  r->name = f[0];
+  r->minus = f[4] == "-";
+  if (r->minus) { const int64_t a = qlen - qe, c = qlen - qs; qs = a; qe = c; }  // :226-228
+  if (!have_cs) { *err = "IndexError: no cs: tag"; return MPC_INGEST_ERROR; }
+  r->cs = cs;
+  r->qs = qs; r->qe = qe; r->ts = ts;
+  return MPC_INGEST_OK;
+}
+
+// Python s[:k] / s[k:] bounds for a string of length L
+inline int64_t py_cut(int64_t L, int64_t k) {
+  if (k < 0) k += L;
+  return k < 0 ? 0 : (k > L ? L : k);
+}
+
+struct Flank {
+  size_t pos = SIZE_MAX;  // file position of the record (duplicates: the last wins)
+  std::string up, down;
+};
+
+}  // namespace
+
+extern "C" {
+
+int mpc_ingest_version(void) { return 1; }
+
+void mpc_ingest_free(mpc_ingest_out* o) {
+  if (!o) return;
+  free(o->ref); free(o->cs); free(o->cs_off); free(o->tstart); free(o->up); free(o->up_off);
+  free(o->down); free(o->down_off); free(o->aligned);
+  o->ref = o->cs = o->up = o->down = nullptr;
+  o->cs_off = o->tstart = o->up_off = o->down_off = o->aligned = nullptr;
+}
+
+int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_path, int n_threads,
+               mpc_ingest_out* out) {
+  memset(out, 0, sizeof(*out));
+  auto finish = [&](int code, const std::string& msg) {
+    out->status = code;
+    snprintf(out->message, sizeof(out->message), "%s", msg.c_str());
+    if (code != MPC_INGEST_OK) mpc_ingest_free(out);
+    return code;
+  };
+  unsigned hw = std::thread::hardware_concurrency();
+  const int T = std::max(1, std::min(n_threads > 0 ? n_threads : (int)(hw ? hw : 4), 64));
+  Mapped fr, fp, fa;
+  if (!fr.open(ref_path)) return finish(MPC_INGEST_ERROR, std::string("cannot open ") + ref_path);
+  if (!fp.open(paf_path)) return finish(MPC_INGEST_ERROR, std::string("cannot open ") + paf_path);
+  if (!fa.open(reads_path)) return finish(MPC_INGEST_ERROR, std::string("cannot open ") + reads_path);
+  if (needs_python(fr, T) || needs_python(fp, T) || needs_python(fa, T))
+    return finish(MPC_INGEST_FALLBACK, "non-ASCII byte or carriage return: Python text-mode semantics");
+
+  // ---- Step 1: reference (:161-184) ----
+  std::string ref;
+  ref.reserve(fr.n);
+  for (size_t a = 0; a < fr.n;) {
+    const char* nl = static_cast<const char*>(memchr(fr.p + a, '\n', fr.n - a));
+    const size_t e = nl ? (size_t)(nl - fr.p) : fr.n;
+    const sv line(fr.p + a, e - a);
+    if (line.empty() || line[0] != '>')
+      for (char c : rstrip(line)) ref.push_back(upper(c));
+    a = e + 1;
+  }
+
+  // ---- Step 2: PAF (:192-245), chunks of lines in parallel, dedup in file order ----
+  std::vector<std::vector<PafRec>> recs(T);
+  std::vector<Fail> fails(T);
+  std::vector<int64_t> nlines(T, 0);
+  parallel(T, [&](int k) {
+    const size_t a = line_start_at_or_after(fp, fp.n * k / T), b = line_start_at_or_after(fp, fp.n * (k + 1) / T);
+    for (size_t x = a; x < b;) {
+      const char* nl = static_cast<const char*>(memchr(fp.p + x, '\n', b - x));
+      const size_t e = nl ? (size_t)(nl - fp.p) : b;
+      PafRec r;
+      std::string err;
+      ++nlines[k];
+      const int rc = parse_paf_line(sv(fp.p + x, e - x), &r, &err);
+      if (rc == MPC_INGEST_OK) recs[k].push_back(r);
+      else fails[k].set(rc, x, rc == MPC_INGEST_ERROR ? "PAF line: " + err : std::string("PAF integer field for Python"));
+      x = e + 1;
+    }
+  });
+  Fail fail;
+  for (auto& f : fails) fail.merge(f);
+  if (fail.code != MPC_INGEST_OK) return finish(fail.code, fail.msg);
+  int64_t n_lines = 0;
+  size_t total = 0;
+  for (int k = 0; k < T; ++k) { n_lines += nlines[k]; total += recs[k].size(); }
+  std::vector<PafRec> keep;
+  keep.reserve(total);
+  std::unordered_map<sv, int64_t> by_name;
+  by_name.reserve(total * 2 + 16);
+  for (int k = 0; k < T; ++k)
+    for (const PafRec& r : recs[k])
+      if (by_name.emplace(r.name, (int64_t)keep.size()).second) keep.push_back(r);  // first line wins (:237-243)
+  recs.clear();
+  const int64_t N = (int64_t)keep.size();
+
+  // ---- Step 3: reads FASTA (:253-277), chunks of records in parallel ----
+  std::vector<Flank> flanks(N);
+  std::mutex locks[64];
+  std::vector<Fail> ffails(T);
+  auto rec_start = [&](size_t x) {  // first header line ('>' at a line start) at or after x
+    size_t y = line_start_at_or_after(fa, x);
+    while (y < fa.n && fa.p[y] != '>') {
+      const char* nl = static_cast<const char*>(memchr(fa.p + y, '\n', fa.n - y));
+      y = nl ? (size_t)(nl - fa.p) + 1 : fa.n;
+    }
+    return y;
+  };
+  parallel(T, [&](int k) {
+    const size_t a = k == 0 ? 0 : rec_start(fa.n * k / T), b = k == T - 1 ? fa.n : rec_start(fa.n * (k + 1) / T);
+    std::string seq, rc;
+    int64_t cur = -1;        // record of the current name, -1: not in the PAF (or before the first header)
+    size_t cur_pos = 0;
+    auto done = [&]() {      // :259-265 for the record just read
+      if (cur < 0) return;
+      const PafRec& r = keep[cur];
+      const std::string* s = &seq;
+      if (r.minus) {  // "".join([BASE_COMPLIMENT[x.upper()] for x in seq[::-1]]) (:263)
+        rc.resize(seq.size());
+        for (size_t i = 0; i < seq.size(); ++i) {
+          const char c = seq[seq.size() - 1 - i];
+          char o;
+          switch (c) {
+            case 'A': o = 'T'; break; case 'T': o = 'A'; break; case 'G': o = 'C'; break;
+            case 'C': o = 'G'; break; case 'N': o = 'N'; break;
+            default:
+              ffails[k].set(MPC_INGEST_ERROR, cur_pos, "KeyError: '" + std::string(1, c) + "' (reverse complement of read " +
+                                                           std::string(r.name.substr(0, 80)) + ")");
+              return;
+          }
+          rc[i] = o;
+        }
+        s = &rc;
+      }
+      const int64_t L = (int64_t)s->size();
+      const int64_t u = py_cut(L, r.qs), d = py_cut(L, r.qe);
+      std::lock_guard<std::mutex> g(locks[cur & 63]);
+      Flank& fl = flanks[cur];
+      if (fl.pos == SIZE_MAX || cur_pos > fl.pos) {  // a duplicate name: the last record wins
+        fl.pos = cur_pos;
+        fl.up.assign(s->data(), (size_t)u);
+        fl.down.assign(s->data() + d, (size_t)(L - d));
+      }
+    };
+    for (size_t x = a; x < b;) {
+      const char* nl = static_cast<const char*>(memchr(fa.p + x, '\n', b - x));
+      const size_t e = nl ? (size_t)(nl - fa.p) : b;
+      const sv line(fa.p + x, e - x);
+      if (!line.empty() && line[0] == '>') {
+        done();
+        const sv name = rstrip(line).substr(1);  // whole header line (:267); "" is never processed (:260)
+        auto it = name.empty() ? by_name.end() : by_name.find(name);
+        cur = it == by_name.end() ? -1 : it->second;
+        cur_pos = x;
+        seq.clear();
+      } else if (cur >= 0) {
+        for (char c : rstrip(line)) seq.push_back(upper(c));  // :270
+      }
+      x = e + 1;
+    }
+    done();
+  });
+  for (auto& f : ffails) fail.merge(f);
+  if (fail.code != MPC_INGEST_OK) return finish(fail.code, fail.msg);
+
+  // ---- pack in PAF first-occurrence order (:292) ----
+  size_t ncs = 0, nup = 0, ndn = 0;
+  for (int64_t i = 0; i < N; ++i) {
+    if (flanks[i].pos == SIZE_MAX)  // paf[read_name]["upstream_seq"] -> KeyError (:303)
+      return finish(MPC_INGEST_ERROR, "KeyError: 'upstream_seq' (read " + std::string(keep[i].name.substr(0, 80)) +
+                                          " not in the reads file)");
+    if (keep[i].ts < 0 || keep[i].ts >= ((int64_t)1 << 31))
+      return finish(MPC_INGEST_ERROR, "target start out of range (unsupported)");
+    ncs += keep[i].cs.size(); nup += flanks[i].up.size(); ndn += flanks[i].down.size();
+  }
+  auto alloc = [](size_t n) { return malloc(n ? n : 1); };
+  out->ref = (uint8_t*)alloc(ref.size());
+  memcpy(out->ref, ref.data(), ref.size());
+  out->ref_len = (int64_t)ref.size();
+  out->cs = (uint8_t*)alloc(ncs); out->up = (uint8_t*)alloc(nup); out->down = (uint8_t*)alloc(ndn);
+  out->cs_off = (int64_t*)alloc(8 * (N + 1)); out->up_off = (int64_t*)alloc(8 * (N + 1));
+  out->down_off = (int64_t*)alloc(8 * (N + 1));
+  out->tstart = (int64_t*)alloc(8 * N); out->aligned = (int64_t*)alloc(8 * N);
+  size_t oc = 0, ou = 0, od = 0;
+  for (int64_t i = 0; i < N; ++i) {
+    out->cs_off[i] = (int64_t)oc; out->up_off[i] = (int64_t)ou; out->down_off[i] = (int64_t)od;
+    memcpy(out->cs + oc, keep[i].cs.data(), keep[i].cs.size()); oc += keep[i].cs.size();
+    memcpy(out->up + ou, flanks[i].up.data(), flanks[i].up.size()); ou += flanks[i].up.size();
+    memcpy(out->down + od, flanks[i].down.data(), flanks[i].down.size()); od += flanks[i].down.size();
+    out->tstart[i] = keep[i].ts;
+    out->aligned[i] = keep[i].qe - keep[i].qs;
+  }
+  out->cs_off[N] = (int64_t)oc; out->up_off[N] = (int64_t)ou; out->down_off[N] = (int64_t)od;
+  out->n_reads = N;
+  out->n_alignments = n_lines;
+  return finish(MPC_INGEST_OK, "");
+}
+
+}  // extern "C"

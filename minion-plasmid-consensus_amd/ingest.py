@@ -10,7 +10,16 @@ writes nothing, like the reference).
   Step 1  reference FASTA       :161-184  -> read_reference()
   Step 2  PAF                   :192-245  -> read_paf()
   Step 3  reads FASTA + flanks  :253-277  -> read_flanks()
+
+``pack_sample`` uses the native parser (libmpc_ingest.so, include/mpc_ingest.h:
+memory-mapped, multi-threaded, same results) and falls back to the Python
+restatement below when the native library declines an input feature it does
+not restate (non-ASCII bytes, carriage returns, integers in a form only
+Python's int() accepts) or is not built.
 """
+import ctypes
+import os
+
 import numpy as np
 
 BASE_COMPLIMENT = {"A": "T", "T": "A", "G": "C", "C": "G", "N": "N"}  # :27
@@ -118,8 +127,91 @@ def _concat(items):
     return b"".join(items), off
 
 
-def pack_sample(ref_path, paf_path, reads_path):
-    """Steps 1-3 for one (assembly, PAF) sample -> dict of packed numpy arrays."""
+class _IngestOut(ctypes.Structure):
+    _fields_ = [
+        ("ref", ctypes.POINTER(ctypes.c_uint8)), ("ref_len", ctypes.c_int64),
+        ("cs", ctypes.POINTER(ctypes.c_uint8)), ("cs_off", ctypes.POINTER(ctypes.c_int64)),
+        ("tstart", ctypes.POINTER(ctypes.c_int64)),
+        ("up", ctypes.POINTER(ctypes.c_uint8)), ("up_off", ctypes.POINTER(ctypes.c_int64)),
+        ("down", ctypes.POINTER(ctypes.c_uint8)), ("down_off", ctypes.POINTER(ctypes.c_int64)),
+        ("aligned", ctypes.POINTER(ctypes.c_int64)),
+        ("n_reads", ctypes.c_int64), ("n_alignments", ctypes.c_int64),
+        ("status", ctypes.c_int32), ("message", ctypes.c_char * 256),
+    ]
+
+
+INGEST_OK, INGEST_ERROR, INGEST_FALLBACK = 0, 1, 2
+_ingest_lib = None
+
+
+def _native():
+    global _ingest_lib
+    if _ingest_lib is None:
+        from . import _build
+        path = _build.LIBINGEST
+        if not os.path.exists(path):
+            try:
+                _build.build_ingest()
+            except Exception:  # no compiler: the Python ingest is used
+                _ingest_lib = False
+                return None
+        L = ctypes.CDLL(path)
+        L.mpc_ingest.restype = ctypes.c_int
+        L.mpc_ingest.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
+                                 ctypes.POINTER(_IngestOut)]
+        L.mpc_ingest_free.argtypes = [ctypes.POINTER(_IngestOut)]
+        _ingest_lib = L
+    return _ingest_lib or None
+
+
+def pack_sample_native(ref_path, paf_path, reads_path, n_threads=0):
+    """Steps 1-3 through libmpc_ingest.so.  Returns the packed dict, None when the
+    native parser declines the input (use :func:`pack_sample_python`), or raises
+    :class:`IngestError` where the reference raises."""
+    L = _native()
+    if L is None:
+        return None
+    o = _IngestOut()
+    enc = lambda p: os.fsencode(p)
+    L.mpc_ingest(enc(ref_path), enc(paf_path), enc(reads_path), int(n_threads), ctypes.byref(o))
+    try:
+        if o.status == INGEST_FALLBACK:
+            return None
+        if o.status != INGEST_OK:
+            raise IngestError(o.message.decode(errors="replace"))
+        n = o.n_reads
+
+        def arr(p, k, dt):
+            return np.ctypeslib.as_array(p, shape=(k,)).astype(dt, copy=True) if k else np.zeros(0, dtype=dt)
+
+        cs_off = arr(o.cs_off, n + 1, np.int64)
+        up_off = arr(o.up_off, n + 1, np.int64)
+        dn_off = arr(o.down_off, n + 1, np.int64)
+        return dict(
+            ref=arr(o.ref, o.ref_len, np.uint8),
+            cs=arr(o.cs, int(cs_off[-1]), np.uint8), cs_off=cs_off,
+            tstart=arr(o.tstart, n, np.int64),
+            up=arr(o.up, int(up_off[-1]), np.uint8), up_off=up_off,
+            down=arr(o.down, int(dn_off[-1]), np.uint8), down_off=dn_off,
+            aligned=arr(o.aligned, n, np.int64),
+            n_alignments=int(o.n_alignments),
+        )
+    finally:
+        L.mpc_ingest_free(ctypes.byref(o))
+
+
+def pack_sample(ref_path, paf_path, reads_path, native=True):
+    """Steps 1-3 for one (assembly, PAF) sample -> dict of packed numpy arrays
+    (native parser when it accepts the input, else the Python restatement)."""
+    if native:
+        r = pack_sample_native(ref_path, paf_path, reads_path)
+        if r is not None:
+            return r
+    return pack_sample_python(ref_path, paf_path, reads_path)
+
+
+def pack_sample_python(ref_path, paf_path, reads_path):
+    """Steps 1-3 for one (assembly, PAF) sample in Python -> dict of packed numpy arrays."""
     refseq = read_reference(ref_path)
     recs, n_lines = read_paf(paf_path)
     flanks = read_flanks(reads_path, recs)

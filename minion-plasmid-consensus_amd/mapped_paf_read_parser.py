@@ -76,7 +76,7 @@ def main(argv=None):
         results = engine.pileup(samples, args.MIN_DEPTH_FACTOR, 1.0 if gtf is None else gtf, device=args.device)
         if gtf is None and any(len(r["count"]) or r["max_depth"] for r in results):
             raise ingest.IngestError("TypeError: --global_threshold_factor is required")  # (:421)
-    except (ingest.IngestError, engine.DataError, OSError) as e:
+    except (ingest.IngestError, engine.DataError, OSError, UnicodeDecodeError) as e:
         print("Error: {}".format(e), file=sys.stderr)
         return 1
     for (ref, paf, c, ch, acc), res in zip(jobs, results):

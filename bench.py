@@ -44,7 +44,13 @@ CONFIGS = {
            "C3 (BASELINE configs[2]): 10 kb plasmid, 1M reads total over 8 GPUs (125k per GPU), sense"),
     "c4": (10_000, 100_000, "indel", 4, True,
            "C4 (BASELINE configs[3]): 10 kb, 100k reads, indel-heavy 1/5/5 %, sense+antisense"),
+    # multi-sample: 96 plasmids partitioned over the ranks (12 per GPU at N=8), both strands,
+    # replicas only (no collective); at N=1 one GPU holds the 12 plasmids of rank 0
+    "c5": (30_000, 10_000, "default", 5000, True,
+           "C5 (BASELINE configs[4]): 30 kb BAC-size constructs, 12 plasmids x 10k reads per GPU "
+           "(96 over 8 GPUs), sense+antisense, sample-partitioned"),
 }
+C5_PER_GPU = 12
 
 
 def main():
@@ -80,10 +86,16 @@ def main():
     eng = pkg.engine
 
     n, reads, profile, seed, antisense, desc = CONFIGS[args.config]
-    # every rank generates its own contiguous shard of the global read list
-    syn = pkg.synth.Synth(n=n, n_reads=reads, profile=profile, seed=seed + 7919 * rank, antisense=antisense)
-    samples = [syn.sample(s) for s in range(2 if antisense else 1)]
-    if world > 1:
+    if args.config == "c5":  # this rank's plasmids (distinct references), both strands
+        samples = []
+        for k in range(C5_PER_GPU):
+            syn = pkg.synth.Synth(n=n, n_reads=reads, profile=profile, seed=seed + C5_PER_GPU * rank + k,
+                                  antisense=antisense)
+            samples += [syn.sample(s) for s in range(2 if antisense else 1)]
+    else:  # every rank generates its own contiguous shard of the global read list
+        syn = pkg.synth.Synth(n=n, n_reads=reads, profile=profile, seed=seed + 7919 * rank, antisense=antisense)
+        samples = [syn.sample(s) for s in range(2 if antisense else 1)]
+    if world > 1 and args.config != "c5":
         dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
         runner = dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange())
     else:

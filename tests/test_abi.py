@@ -7,9 +7,9 @@ import re
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared():
-    txt = open(os.path.join(REPO, "include", "mpc.h")).read()
-    return sorted(set(re.findall(r"^(?:int|const char\*)\s+(mpc_\w+)\(", txt, re.M)))
+def declared(header="mpc.h"):
+    txt = open(os.path.join(REPO, "include", header)).read()
+    return sorted(set(re.findall(r"^(?:int|void|const char\*)\s+(mpc_\w+)\(", txt, re.M)))
 
 
 def test_header_declares_entry_points():
@@ -36,3 +36,12 @@ def test_no_oracle_in_product():
             if f.endswith((".py", ".hip", ".cpp", ".h")):
                 src = open(os.path.join(root, f), errors="replace").read()
                 assert "import oracle" not in src and "mpc_oracle" not in src, f
+
+
+def test_ingest_library_exports_all(pkg):
+    path = pkg._build.build_ingest()
+    lib = ctypes.CDLL(path)
+    names = declared("mpc_ingest.h")
+    assert "mpc_ingest" in names and "mpc_ingest_free" in names
+    for name in names:
+        assert hasattr(lib, name), name

@@ -9,6 +9,9 @@ Extra, optional flags (defaults keep the reference behaviour):
   --also REF PAF CONSENSUS CHROMAT ACCURACIES
                      run another (assembly, PAF) pair against the same --reads in
                      the SAME launch (e.g. the antisense strand); repeatable
+  --revcomp SRC DST  after writing, reverse-complement consensus SRC into DST
+                     (Snakefile rule revcomp_antisense_consensus, :425-450);
+                     repeatable
 """
 import argparse
 import importlib
@@ -49,6 +52,8 @@ def build_parser():
     p.add_argument("--also", nargs=5, action="append", default=[],
                    metavar=("REF", "PAF", "CONSENSUS", "CHROMAT", "ACCURACIES"),
                    help="additional (assembly, PAF) job against the same reads, same launch")
+    p.add_argument("--revcomp", nargs=2, action="append", default=[], metavar=("SRC", "DST"),
+                   help="reverse-complement a written consensus file (rule revcomp_antisense_consensus)")
     return p
 
 
@@ -84,6 +89,13 @@ def main(argv=None):
         statprint("DEPTH_THRESHOLD is {}.".format(res["max_depth"] * args.MIN_DEPTH_FACTOR))
         statprint("Writing consensus, chromatogram data and per-position consensus accuracies...")
         writers.write_outputs(res, c, ch, acc)
+    for src, dst in args.revcomp:
+        statprint("Reverse-complementing {} into {}...".format(src, dst))
+        try:
+            writers.revcomp_consensus(src, dst)
+        except (writers.RevcompError, OSError, UnicodeDecodeError) as e:
+            print("Error: {}".format(e), file=sys.stderr)
+            return 1
     statprint("Done.")
     return 0
 

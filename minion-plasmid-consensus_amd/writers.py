@@ -42,3 +42,43 @@ def write_outputs(calls, consensus_path, chromat_path, accuracies_path):
         f.write(chromat_text(calls))
     with open(accuracies_path, "w") as f:
         f.write(accuracies_text(calls))
+
+
+# Snakefile:77 (the rule's own table; no lower case, no 'X')
+_COMPLEMENT = {"A": "T", "T": "A", "G": "C", "C": "G", "N": "N"}
+
+
+class RevcompError(ValueError):
+    pass
+
+
+def revcomp_text(lines):
+    """Rule `revcomp_antisense_consensus` (Snakefile:425-450) on a list of lines
+    (each with its newline, as file iteration yields them): every '>' line is
+    copied; then the reverse complement of the LAST line only (rstripped,
+    upper-cased) is appended without a newline (:445, the rule uses the loop
+    variable, not the accumulated sequence).  Returns (text, error): on a base
+    outside A/C/G/T/N or an empty file the rule raises after the header lines
+    were written, so the partial text is returned with the error."""
+    head = "".join(ln for ln in lines if ln.startswith(">"))
+    if not lines:
+        return head, RevcompError("NameError: name 'line' is not defined")  # empty input: loop never ran
+    out = []
+    for x in lines[-1].rstrip()[::-1]:
+        c = _COMPLEMENT.get(x.upper())
+        if c is None:
+            return head, RevcompError("KeyError: {!r}".format(x.upper()))
+        out.append(c)
+    return head + "".join(out), None
+
+
+def revcomp_consensus(src_path, dst_path):
+    """File form of revcomp_text; raises RevcompError like the rule (exit 1)
+    after writing the header lines."""
+    with open(src_path, "r") as f:
+        lines = f.readlines()
+    text, err = revcomp_text(lines)
+    with open(dst_path, "w") as f:
+        f.write(text)
+    if err is not None:
+        raise err

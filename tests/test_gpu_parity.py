@@ -40,6 +40,34 @@ def test_cli_matches_reference(case, tmp_path, cli):
             assert not any(os.path.exists(o) for o in outs), "no partial outputs on failure"
 
 
+@pytest.mark.parametrize("stem", ["r01_default", "r03_indel"])
+def test_cli_both_strands_one_launch(stem, tmp_path, cli):
+    """--also (sense + antisense in one launch, same reads file) and --revcomp
+    (rule revcomp_antisense_consensus): every file equals the golden per-strand
+    outputs of the reference, the revcomp file the rule applied to them."""
+    (ts, s), (ta, a) = [(tmp_path / x, f"{stem}_{x}") for x in ("sense", "antisense")]
+    ts.mkdir()
+    ta.mkdir()
+    ref_s, reads, paf_s = gu.materialize(s, str(ts))
+    ref_a, _, paf_a = gu.materialize(a, str(ta))
+    for (k, run, exp_s), (_, run_a, exp_a) in zip(gu.runs(s), gu.runs(a)):
+        assert (run["mdf"], run["gtf"]) == (run_a["mdf"], run_a["gtf"])
+        o_s = [str(ts / f"o{k}_{x}") for x in ("c.fa", "ch.tsv", "acc.tsv")]
+        o_a = [str(ta / f"o{k}_{x}") for x in ("c.fa", "ch.tsv", "acc.tsv")]
+        rc_path = str(ta / f"o{k}_rc.fa")
+        rc = cli.main(["--ref", ref_s, "--reads", reads, "--paf", paf_s, "--consensus", o_s[0], "--chromat", o_s[1],
+                       "--accuracies", o_s[2], "--min_depth_factor", repr(run["mdf"]),
+                       "--global_threshold_factor", repr(run["gtf"]), "--also", ref_a, paf_a, *o_a,
+                       "--revcomp", o_a[0], rc_path])
+        assert rc == 0, (stem, k)
+        for outs, exp in ((o_s, exp_s), (o_a, exp_a)):
+            for o, f in zip(outs, ("c.fa", "ch.tsv", "acc.tsv")):
+                assert open(o, "rb").read() == exp[f], (stem, k, f)
+        seq = exp_a["c.fa"].decode().split("\n")[1]
+        comp = {"A": "T", "T": "A", "C": "G", "G": "C", "N": "N"}
+        assert open(rc_path).read() == ">consensus\n" + "".join(comp[b] for b in reversed(seq))
+
+
 def _oracle(s, mdf, gtf):
     return oracle.run_packed(s["ref"], s["cs"], s["cs_off"], s["tstart"], s["up"], s["up_off"], s["down"],
                              s["down_off"], mdf, gtf)

@@ -157,7 +157,8 @@ struct alignas(16) WaveLds {            // per-wave LDS of K_parse
   uint8_t stage[WIN + 16];              // window bytes (+16: word reads past the end)
   uint8_t em[WIN / 8];                  // boundary bits (special characters | read starts), bit = byte
   uint8_t ra[WIN / 8];                  // read-start bits
-  uint16_t tok[WIN + 2 + 64];           // token starts in [P, C), then the sentinel C; bit 15 = read start (+64: unconditional loads)
+  uint16_t tok[WIN + 2 + 64];           // unit starts in [P, C), then the sentinel C; bits 12-14: ':' prefix
+                                        // operand length, bit 15: read start (+64: unconditional loads)
 };
 
 struct ParseArgs {  // slim argument block (no SGPR spills)
@@ -261,6 +262,35 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
+// ':' bits and op ('*', '+', '-') bits of a lane's CH staged bytes
+template <int CH>
+__device__ __forceinline__ void class_masks(const uint32_t* w, uint32_t* cm, uint32_t* om) {
+  uint32_t c_ = 0, o_ = 0;
+#pragma unroll
+  for (int k = 0; k < CH; ++k) {
+    const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+    c_ |= (uint32_t)(c == 0x3Au) << k;
+    o_ |= (uint32_t)(((c - 0x2Au) <= 3u) & (c != 0x2Cu)) << k;
+  }
+  *cm = c_;
+  *om = o_;
+}
+__device__ __forceinline__ void class_masks(uint4 v, uint32_t* cm, uint32_t* om) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  class_masks<16>(w, cm, om);
+}
+__device__ __forceinline__ void class_masks(uint2 v, uint32_t* cm, uint32_t* om) {
+  const uint32_t w[2] = {v.x, v.y};
+  class_masks<8>(w, cm, om);
+}
+// lane l gets x of lane l-1 (0 on lane 0) / of lane l+1 (0 on lane 63)
+__device__ __forceinline__ uint32_t from_lane_below(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x138, 0xf, 0xf, true);  // wave_shr:1
+}
+__device__ __forceinline__ uint32_t from_lane_above(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);  // wave_shl:1
+}
+
 // special-character bits of a lane's 8 staged bytes
 __device__ __forceinline__ uint32_t special_mask8(uint2 v) {
   const uint32_t w[2] = {v.x, v.y};
@@ -309,11 +339,13 @@ __device__ __forceinline__ void chunk_store(uint8_t* p, uint2 v) { *reinterpret_
 // processed).  Token boundaries (special characters and read starts) are bits
 // of an LDS mask.  A window is cut at its LAST boundary C, so every token in
 // [P, C) ends inside the window (no lookahead halo); the next window starts at
-// C.  The token starts are compacted into a list and processed ONE TOKEN PER
-// LANE, 64 per round: branch-free SWAR decode of the operand word, one DPP
-// scan of the advances for the coordinates i (reads are segments: per-read
-// bases in a slot table), ballot/mbcnt for the read slot and the insertion
-// event index.  Effects: substitution / deletion / span tallies (LDS, 12 B per
+// C.  The token starts are compacted into a list of UNITS -- a ':' token
+// with 1-4 digits and the op token right after it in the same read form one
+// unit (minimap2's short cs alternates them, so this halves the list) -- and
+// processed ONE UNIT PER LANE, 64 per round: branch-free SWAR decode of the
+// operand words, one DPP scan of the advances for the coordinates i (reads
+// are segments: per-read bases in a slot table), ballot/mbcnt for the read
+// slot and the insertion event index.  Effects: substitution / deletion / span tallies (LDS, 12 B per
 // position), insertion events (stored straight into the wave's region of
 // ins_raw), LEFT-gap bits (LDS bitmap).  Epilogue: flush tallies, bucket-sort
 // the insertion events by gap.
@@ -476,15 +508,44 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       tlo = tlo < 0 ? 0 : (tlo > CH ? CH : tlo);
       thi = thi < 0 ? 0 : (thi > CH ? CH : thi);
       const uint32_t tm = em_own & ((1u << thi) - 1u) & ~((1u << tlo) - 1u);
-      const int cnt = __popc(tm);
+      // Units: a ':' token with 1-4 operand bytes and the op token ('*', '+',
+      // '-') right after it in the same read, both in [P, C), are ONE list
+      // entry (bits 12-14: the ':' operand length); every other token is its
+      // own entry.  Bit-parallel over this lane's bytes and its neighbours'
+      // (DPP wave shifts): bit CH + k of a 3-lane mask = own byte k.
+      uint32_t cm_own, om_own;
+      class_masks(cur.d, &cm_own, &om_own);
+      const uint32_t rng = ((1u << thi) - 1u) & ~((1u << tlo) - 1u);
+      const uint32_t cmr = cm_own & rng, omr = om_own & ~ra_own & rng;
+      const uint64_t em3 = (uint64_t)from_lane_below(em_own) | ((uint64_t)em_own << CH) |
+                           ((uint64_t)from_lane_above(em_own) << (2 * CH));
+      const uint64_t cm3 = (uint64_t)from_lane_below(cmr) | ((uint64_t)cmr << CH) |
+                           ((uint64_t)from_lane_above(cmr) << (2 * CH));
+      const uint64_t om3 = ((uint64_t)omr << CH) | ((uint64_t)from_lane_above(omr) << (2 * CH));
+      const uint64_t nb1 = ~(em3 << 1), nb12 = nb1 & ~(em3 << 2), nb123 = nb12 & ~(em3 << 3);
+      const uint64_t c2 = (cm3 << 2) & nb1;                   // ':' 2 bytes before, no boundary between
+      const uint64_t c3 = (cm3 << 3) & nb12;
+      const uint64_t c4 = (cm3 << 4) & nb123;
+      const uint64_t c5 = (cm3 << 5) & nb123 & ~(em3 << 4);
+      const uint64_t ab = om3 & (c2 | c3 | c4 | c5);          // absorbed ops
+      const uint32_t own = CH == 16 ? 0xffffu : 0xffu;
+      const uint32_t p2 = (uint32_t)(((ab & c2) >> (CH + 2))) & own;  // ':' whose op is 2 bytes on
+      const uint32_t p3 = (uint32_t)(((ab & c3) >> (CH + 3))) & own;
+      const uint32_t p4 = (uint32_t)(((ab & c4) >> (CH + 4))) & own;
+      const uint32_t p5 = (uint32_t)(((ab & c5) >> (CH + 5))) & own;
+      const uint32_t pl0 = p2 | p4, pl1 = p3 | p4;            // operand length d - 1 in 3 bit planes
+      const uint32_t tu = tm & ~((uint32_t)(ab >> CH) & own);
+      const int cnt = __popc(tu);
       const int incl = wave_scan_i32(cnt);
       T = wave_last_i32(incl);
       int idx = incl - cnt;
-      uint32_t m = tm;
+      const int base = CH * l;
+      uint32_t m = tu;
       while (m) {
         const int k = __ffs(m) - 1;
         m &= m - 1;
-        W.tok[idx++] = (uint16_t)((CH * l + k) | (((ra_own >> k) & 1u) << 15));
+        W.tok[idx++] = (uint16_t)((uint32_t)(base + k) | (((pl0 >> k) & 1u) << 12) | (((pl1 >> k) & 1u) << 13) |
+                                  (((p5 >> k) & 1u) << 14) | (((ra_own >> k) & 1u) << 15));
       }
       if (l == 0) W.tok[T] = far ? (uint16_t)(kFar | (c_rs ? 0x8000u : 0u)) : (uint16_t)((C - A) | (c_rs ? 0x8000u : 0u));
     }
@@ -497,10 +558,13 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     for (int t0 = 0; t0 < T; t0 += 64) {
       const int t = t0 + l;
       const bool v = t < T;
-      const uint32_t e0 = v ? W.tok[t] : 0u, e1 = v ? W.tok[t + 1] : 0u;
-      const int sx = (int)(e0 & 0x7fffu);
+      const uint32_t t0r = W.tok[t], t1r = W.tok[t + 1];  // in bounds for every lane (+64 padding)
+      const uint32_t e0 = v ? t0r : 0u, e1 = v ? t1r : 0u;
+      const int s0 = (int)(e0 & 0xfffu);         // unit start
+      const int pl = (int)((e0 >> 12) & 7u);     // ':' operand length of a unit's prefix (0: none)
+      const int sx = pl ? s0 + pl + 1 : s0;      // the unit's main token
       const bool lfar = v && ((e1 & 0x7fffu) == kFar);
-      const int64_t ex64 = lfar ? C - A : (int64_t)(e1 & 0x7fffu);  // far: the token ends at C (beyond the window)
+      const int64_t ex64 = lfar ? C - A : (int64_t)(e1 & 0xfffu);  // far: the token ends at C (beyond the window)
       const int ex = (int)(ex64 - sx - 1 < kAdvCap ? ex64 : sx + 1 + kAdvCap);
       const bool is_rs = v && (e0 >> 15);
       const bool last = v && (e1 >> 15);
@@ -541,7 +605,17 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       pk = (pk | (pk >> 6)) & 0x000f000fu;
       pk = (pk | (pk >> 12)) & 0xffu;
       uint32_t pay = star ? ((codes >> shl) & 3u) : (pk & ((1u << (2 * ol4)) - 1u));
-      const bool slow = lfar | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));
+      //   prefix ':' operand (pl bytes after s0)
+      const int pa = (s0 + 1) >> 2;
+      const uint32_t pw = __builtin_amdgcn_alignbyte(b32[pa + 1], b32[pa], (uint32_t)((s0 + 1) & 3));
+      const uint32_t pvm = pl == 0 ? 0u : pl == 4 ? 0xffffffffu : ((1u << (8 * pl)) - 1u);
+      const uint32_t pT = pw ^ 0x30303030u;
+      const uint32_t pnd = (((pT & 0x7F7F7F7Fu) + 0x76767676u) | pT) & 0x80808080u;
+      uint32_t pX = pl == 0 ? 0u : (pT & pvm & 0x0F0F0F0Fu) << (8 * (4 - pl));
+      pX = (pX * 2561u) >> 8;
+      pX = ((pX & 0x00FF00FFu) * 6553601u) >> 16;
+      int adv0 = (int)(pX & 0xffffu);
+      const bool slow = lfar | (v & ((pnd & pvm) != 0)) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));
       int kind = !act ? 0 : colon ? (adv_c > 0 ? 1 : 0) : (olen <= 0) ? 0 : star ? 2 : plus ? 3 : minus ? 4 : 0;
       int adv = kind == 1 ? adv_c : kind == 2 ? 1 : kind == 4 ? (olen < kAdvCap ? olen : kAdvCap) : 0;
       uint32_t err = (v & !spec) ? DE_OP : 0u;  // cs does not start with an operator (:100-102)
@@ -554,16 +628,24 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         const TokInfo ti = analyze_long(a.cs, s, e, last);
         adv = ti.adv; kind = ti.kind; pay = ti.pay; err = ti.err;
         olen_e = (int)(e - s - 1 < kAdvCap ? e - s - 1 : kAdvCap);
+        if (pl) {
+          const TokInfo tp = analyze_long(a.cs, A + s0, s, false);
+          adv0 = tp.adv;
+          err |= tp.err;
+        }
       }
       // ---- coordinates ----
-      const int ainc = wave_scan_i32(adv);  // adv <= 2^20: 64 lanes stay < 2^31
-      const int aex = ainc - adv;
+      const int advu = adv0 + adv;            // unit advance <= 2^21: 64 lanes stay < 2^31
+      const int ainc = wave_scan_i32(advu);
+      const int aex = ainc - advu;
       const int atot = wave_last_i32(ainc);
       if (is_rs) W.s_val[q] = W.s_ts[q] - (G + aex);
       wave_sync_lds();
-      const int i = W.s_val[q] + G + aex;
+      const int iu = W.s_val[q] + G + aex;    // coordinate at the unit start
+      const int i = iu + adv0;                // ... and at its main token
       // ---- effects ----
       uint32_t te = err;
+      if (adv0 > 0 && (iu < 0 || i > n)) te |= DE_INDEX;  // prefix ':' writes refarr[2 iu + 1 ...] (:75-80)
       if (kind == 1 && (i < 0 || i + adv > n)) te |= DE_INDEX;
       if (kind == 2 && (uint32_t)i >= (uint32_t)n) te |= DE_INDEX;
       if (kind == 3 && (uint32_t)i > (uint32_t)n) te |= DE_INDEX;

@@ -134,6 +134,15 @@ __device__ __forceinline__ uint32_t special_mask16(uint4 v, int lo, int hi) {
   return m & ((1u << hi) - 1u) & ~((1u << lo) - 1u);
 }
 
+// x * 2561 (= 2^11 + 2^9 + 1) as two full-rate shift-adds; the compiler would
+// fold the shifts back into the quarter-rate v_mul_lo_u32
+__device__ __forceinline__ uint32_t mul2561(uint32_t x) {
+  uint32_t y, z;
+  asm("v_lshl_add_u32 %0, %1, 9, %1" : "=v"(y) : "v"(x));
+  asm("v_lshl_add_u32 %0, %1, 11, %2" : "=v"(z) : "v"(x), "v"(y));
+  return z;
+}
+
 __device__ __forceinline__ int64_t readlane64(int64_t x, int j) {
   const int lo = __builtin_amdgcn_readlane((int)(uint32_t)x, j);
   const int hi = __builtin_amdgcn_readlane((int)(uint32_t)((uint64_t)x >> 32), j);
@@ -591,7 +600,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const uint32_t nd = (((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u;
       const bool dig_ok = (olen >= 1) & (olen <= 4) & ((nd & vm) == 0);
       uint32_t X = (Tx & vm & 0x0F0F0F0Fu) << (8 * (4 - ol4));
-      X = (X * 2561u) >> 8;
+      X = mul2561(X) >> 8;
       X = ((X & 0x00FF00FFu) * 6553601u) >> 16;
       const int adv_c = (int)(X & 0xffffu);
       //   bases: (c|0x20) must equal "acgt"[h] with h = (lc>>1)&3 (v_perm table lookup)
@@ -612,7 +621,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const uint32_t pT = pw ^ 0x30303030u;
       const uint32_t pnd = (((pT & 0x7F7F7F7Fu) + 0x76767676u) | pT) & 0x80808080u;
       uint32_t pX = pl == 0 ? 0u : (pT & pvm & 0x0F0F0F0Fu) << (8 * (4 - pl));
-      pX = (pX * 2561u) >> 8;
+      pX = mul2561(pX) >> 8;
       pX = ((pX & 0x00FF00FFu) * 6553601u) >> 16;
       int adv0 = (int)(pX & 0xffffu);
       const bool slow = lfar | (v & ((pnd & pvm) != 0)) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));
@@ -880,13 +889,26 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
     kb[(passes + 1) & 1] = d.keys_tmp; vb[(passes + 1) & 1] = d.vals_tmp;
   }
   __syncthreads();
-  // gather (read order) into buffer 0: one source block per thread (short, independent copies)
+  // gather (read order) into buffer 0: one source block per thread, 8 loads in
+  // flight per batch (the copies are independent; a serial loop would wait a
+  // full memory latency per entry)
   for (int b = tid; b < nblocks; b += kRS) {
     const int c = d.bcnt[b];
     const int o = d.bpre[b];
-    for (int j = 0; j < c; ++j) {
-      kb[0][o + j] = d.keys_in[(int64_t)b * kRS + j];
-      vb[0][o + j] = d.vals_in[(int64_t)b * kRS + j];
+    const uint32_t* ks = d.keys_in + (int64_t)b * kRS;
+    const int32_t* vs = d.vals_in + (int64_t)b * kRS;
+    for (int j0 = 0; j0 < c; j0 += 8) {
+      uint32_t kk[8];
+      int32_t vv[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int j = j0 + u < c ? j0 + u : c - 1;
+        kk[u] = ks[j];
+        vv[u] = vs[j];
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (j0 + u < c) { kb[0][o + j0 + u] = kk[u]; vb[0][o + j0 + u] = vv[u]; }
     }
   }
   __syncthreads();

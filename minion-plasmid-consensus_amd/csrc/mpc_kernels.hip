@@ -156,6 +156,10 @@ constexpr int kSlots = 64;              // reads touching a window (slot 0 = rea
 constexpr int kMaxPW = 16;              // waves per workgroup (runtime: blockDim.x / 64)
 constexpr uint32_t kFar = 0x7fffu;      // sentinel: the window's only token ends beyond the window
 
+// units per window (tok list capacity): a 2 KiB window is cut early when it
+// would hold more (LDS budget), smaller windows never hold more than WIN
+template <int WIN> constexpr int tok_cap() { return WIN <= 1024 ? WIN : 1024; }
+
 template <int WIN>
 struct alignas(16) WaveLds {            // per-wave LDS of K_parse
   int32_t s_val[kSlots];                // i = s_val + (window prefix of advances)
@@ -166,7 +170,7 @@ struct alignas(16) WaveLds {            // per-wave LDS of K_parse
   uint8_t stage[WIN + 16];              // window bytes (+16: word reads past the end)
   uint8_t em[WIN / 8];                  // boundary bits (special characters | read starts), bit = byte
   uint8_t ra[WIN / 8];                  // read-start bits
-  uint16_t tok[WIN + 2 + 64];           // unit starts in [P, C), then the sentinel C; bits 12-14: ':' prefix
+  uint16_t tok[tok_cap<WIN>() + 2 + 64];  // unit starts in [P, C), then the sentinel C; bits 12-14: ':' prefix
                                         // operand length, bit 15: read start (+64: unconditional loads)
 };
 
@@ -271,26 +275,62 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
   return (int)__builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
 }
 
-// ':' bits and op ('*', '+', '-') bits of a lane's CH staged bytes
-template <int CH>
-__device__ __forceinline__ void class_masks(const uint32_t* w, uint32_t* cm, uint32_t* om) {
-  uint32_t c_ = 0, o_ = 0;
+// Per-byte character classes of a lane's staged bytes, SWAR per 32-bit word
+// (no per-byte compares: those pin 2 SGPRs per byte): bit k of sp = byte k is
+// special (: Z * + -), of cm = ':', of om = an op ('*', '+', '-').
+__device__ __forceinline__ uint32_t byte_hits(uint32_t w, uint32_t pat) {  // bit 7 of byte k: byte k == pat's
+  const uint32_t t = w ^ pat;
+  return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
+}
+__device__ __forceinline__ uint32_t hit_nibble(uint32_t z) {  // bits 7, 15, 23, 31 -> bits 0..3
+  z >>= 7;
+  z |= z >> 7;
+  z |= z >> 14;
+  return z & 0xfu;
+}
+template <int NW>
+__device__ __forceinline__ void word_classes(const uint32_t* w, uint32_t* sp, uint32_t* cm, uint32_t* om) {
+  uint32_t s_ = 0, c_ = 0, o_ = 0;
 #pragma unroll
-  for (int k = 0; k < CH; ++k) {
-    const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-    c_ |= (uint32_t)(c == 0x3Au) << k;
-    o_ |= (uint32_t)(((c - 0x2Au) <= 3u) & (c != 0x2Cu)) << k;
+  for (int i = 0; i < NW; ++i) {
+    const uint32_t zc = byte_hits(w[i], 0x3A3A3A3Au);
+    const uint32_t zo = byte_hits(w[i] & 0xFEFEFEFEu, 0x2A2A2A2Au) | byte_hits(w[i], 0x2D2D2D2Du);  // * + | -
+    const uint32_t zs = zc | zo | byte_hits(w[i], 0x5A5A5A5Au);
+    s_ |= hit_nibble(zs) << (4 * i);
+    c_ |= hit_nibble(zc) << (4 * i);
+    o_ |= hit_nibble(zo) << (4 * i);
   }
+  *sp = s_;
   *cm = c_;
   *om = o_;
 }
-__device__ __forceinline__ void class_masks(uint4 v, uint32_t* cm, uint32_t* om) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  class_masks<16>(w, cm, om);
-}
-__device__ __forceinline__ void class_masks(uint2 v, uint32_t* cm, uint32_t* om) {
+struct alignas(16) U8x32 { uint4 a, b; };  // a lane's 32 bytes of a 2 KiB window
+__device__ __forceinline__ void chunk_classes(uint2 v, uint32_t* sp, uint32_t* cm, uint32_t* om) {
   const uint32_t w[2] = {v.x, v.y};
-  class_masks<8>(w, cm, om);
+  word_classes<2>(w, sp, cm, om);
+}
+__device__ __forceinline__ void chunk_classes(uint4 v, uint32_t* sp, uint32_t* cm, uint32_t* om) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  word_classes<4>(w, sp, cm, om);
+}
+__device__ __forceinline__ void chunk_classes(U8x32 v, uint32_t* sp, uint32_t* cm, uint32_t* om) {
+  const uint32_t w[8] = {v.a.x, v.a.y, v.a.z, v.a.w, v.b.x, v.b.y, v.b.z, v.b.w};
+  word_classes<8>(w, sp, cm, om);
+}
+// bits [0, x) set, x in [0, 32]
+__device__ __forceinline__ uint32_t lowmask(int x) { return x >= 32 ? 0xffffffffu : (1u << x) - 1u; }
+// a lane's CH boundary / read-start bits in the per-wave LDS bit arrays
+template <int CH>
+__device__ __forceinline__ void put_lane_bits(uint8_t* arr, int l, uint32_t v) {
+  if (CH == 32) reinterpret_cast<uint32_t*>(arr)[l] = v;
+  else if (CH == 16) reinterpret_cast<uint16_t*>(arr)[l] = (uint16_t)v;
+  else arr[l] = (uint8_t)v;
+}
+template <int CH>
+__device__ __forceinline__ uint32_t get_lane_bits(const uint8_t* arr, int l) {
+  if (CH == 32) return reinterpret_cast<const uint32_t*>(arr)[l];
+  if (CH == 16) return reinterpret_cast<const uint16_t*>(arr)[l];
+  return arr[l];
 }
 // lane l gets x of lane l-1 (0 on lane 0) / of lane l+1 (0 on lane 63)
 __device__ __forceinline__ uint32_t from_lane_below(uint32_t x) {
@@ -300,28 +340,18 @@ __device__ __forceinline__ uint32_t from_lane_above(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x130, 0xf, 0xf, true);  // wave_shl:1
 }
 
-// special-character bits of a lane's 8 staged bytes
-__device__ __forceinline__ uint32_t special_mask8(uint2 v) {
-  const uint32_t w[2] = {v.x, v.y};
-  uint32_t m = 0;
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const uint32_t c = (w[k >> 2] >> (8 * (k & 3))) & 0xffu;
-    const bool sp = (c == 0x3Au) | (c == 0x5Au) | (((c - 0x2Au) <= 3u) & (c != 0x2Cu));  // : Z * + -
-    m |= (uint32_t)sp << k;
-  }
-  return m;
-}
 
 // One window's prefetched inputs: WIN/64 cs bytes per lane and the offsets /
 // tstart of reads rs0 + lane.
 template <int CH> struct Chunk;
 template <> struct Chunk<16> { using T = uint4; };
 template <> struct Chunk<8> { using T = uint2; };
+template <> struct Chunk<32> { using T = U8x32; };
 template <int CH>
 struct WinIn {
   typename Chunk<CH>::T d;
-  int64_t o, uo, dno;
+  int64_t o;
+  uint32_t uo, dno;  // low words of the flank offsets: only the lengths' signs are needed
   int32_t ts;
 };
 template <int CH>
@@ -332,15 +362,17 @@ __device__ __forceinline__ WinIn<CH> fetch_window(const ParseArgs& a, int64_t P,
   const int64_t r = rs0 + l;
   const bool ok = r <= a.n_reads;
   f.o = ok ? a.cs_off[r] : INT64_MAX;
-  f.uo = ok ? a.up_off[r] : 0;
-  f.dno = ok ? a.down_off[r] : 0;
+  f.uo = ok ? reinterpret_cast<const uint32_t*>(a.up_off)[2 * r] : 0u;
+  f.dno = ok ? reinterpret_cast<const uint32_t*>(a.down_off)[2 * r] : 0u;
   f.ts = r < a.n_reads ? a.tstart[r] : 0;
   return f;
 }
-__device__ __forceinline__ uint32_t chunk_mask(uint4 v) { return special_mask16(v, 0, 16); }
-__device__ __forceinline__ uint32_t chunk_mask(uint2 v) { return special_mask8(v); }
 __device__ __forceinline__ void chunk_store(uint8_t* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
 __device__ __forceinline__ void chunk_store(uint8_t* p, uint2 v) { *reinterpret_cast<uint2*>(p) = v; }
+__device__ __forceinline__ void chunk_store(uint8_t* p, U8x32 v) {
+  reinterpret_cast<uint4*>(p)[0] = v.a;
+  reinterpret_cast<uint4*>(p)[1] = v.b;
+}
 
 // Workgroup = contiguous reads of ONE sample (host work table); wave w takes
 // the w-th part of them and streams their cs bytes in windows of WIN bytes
@@ -427,8 +459,8 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     const int64_t o63 = readlane64(cur.o, 63);
     if (o63 < E) E = o63;
     const int64_t o_nx = __shfl(cur.o, (l + 1) & 63, 64);
-    const int64_t uo_nx = __shfl(cur.uo, (l + 1) & 63, 64);
-    const int64_t dno_nx = __shfl(cur.dno, (l + 1) & 63, 64);
+    const uint32_t uo_nx = (uint32_t)__shfl((int)cur.uo, (l + 1) & 63, 64);
+    const uint32_t dno_nx = (uint32_t)__shfl((int)cur.dno, (l + 1) & 63, 64);
     if (E <= P) {
       // reads rs0 .. rs0+62 all start at P: 63 empty cs (processOperation('', ''))
       if (l < 63) {
@@ -441,9 +473,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     }
     // ---- stage bytes, boundary bits ----
     chunk_store(W.stage + CH * l, cur.d);
-    const uint32_t spm = chunk_mask(cur.d);
-    if (CH == 16) reinterpret_cast<uint16_t*>(W.em)[l] = (uint16_t)spm; else W.em[l] = (uint8_t)spm;
-    if (CH == 16) reinterpret_cast<uint16_t*>(W.ra)[l] = 0; else W.ra[l] = 0;
+    uint32_t spm, cm_own, om_own;
+    chunk_classes(cur.d, &spm, &cm_own, &om_own);
+    put_lane_bits<CH>(W.em, l, spm);
+    put_lane_bits<CH>(W.ra, l, 0u);
     wave_sync_lds();
     {  // read-start bits of every read starting inside the window (incl. E)
       const int64_t rel = cur.o - A;
@@ -454,9 +487,8 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     }
     wave_sync_lds();
     const int64_t cA = A + CH * l;
-    const uint32_t cmask = CH == 16 ? 0xffffu : 0xffu;
-    const uint32_t em_own = (CH == 16 ? (uint32_t)reinterpret_cast<const uint16_t*>(W.em)[l] : (uint32_t)W.em[l]) & cmask;
-    const uint32_t ra_own = (CH == 16 ? (uint32_t)reinterpret_cast<const uint16_t*>(W.ra)[l] : (uint32_t)W.ra[l]) & cmask;
+    const uint32_t em_own = get_lane_bits<CH>(W.em, l);
+    const uint32_t ra_own = get_lane_bits<CH>(W.ra, l);
     // ---- cut C: E if E is a boundary (a read start), else the last boundary in (P, E) ----
     const bool e_rs = (E == wend) || (E == o63);
     int64_t C;
@@ -467,7 +499,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       int lo = (int)(P + 1 - cA), hi = (int)(E - cA);
       lo = lo < 0 ? 0 : (lo > CH ? CH : lo);
       hi = hi < 0 ? 0 : (hi > CH ? CH : hi);
-      const uint32_t m = em_own & ((hi >= 32 ? 0xffffffffu : (1u << hi) - 1u)) & ~((1u << lo) - 1u);
+      const uint32_t m = em_own & lowmask(hi) & ~lowmask(lo);
       const uint64_t b = ballot(m != 0);
       if (b) {
         const int f = 63 - __clzll((long long)b);
@@ -487,23 +519,41 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         far = true;
       }
     }
+    if (WIN > tok_cap<WIN>() && !far) {
+      // more than tok_cap tokens in [P, C): cut at the tok_cap-th boundary after P
+      int lo = (int)(P - cA), hi = (int)(C - cA);
+      lo = lo < 0 ? 0 : (lo > CH ? CH : lo);
+      hi = hi < 0 ? 0 : (hi > CH ? CH : hi);
+      const uint32_t m = em_own & lowmask(hi) & ~lowmask(lo);
+      const int cb = __popc(m);
+      const int inc = wave_scan_i32(cb);
+      if (wave_last_i32(inc) > tok_cap<WIN>()) {
+        const int f = __ffsll((unsigned long long)ballot(inc > tok_cap<WIN>())) - 1;
+        uint32_t mf = (uint32_t)__builtin_amdgcn_readlane((int)m, f);
+        const int j = tok_cap<WIN>() - (__builtin_amdgcn_readlane(inc, f) - __builtin_amdgcn_readlane(cb, f));
+        for (int u = 0; u < j; ++u) mf &= mf - 1;  // drop the j lowest boundaries of lane f
+        const int k = __ffs(mf) - 1;
+        C = A + CH * f + k;
+        c_rs = (((uint32_t)__builtin_amdgcn_readlane((int)ra_own, f)) >> k) & 1u;
+      }
+    }
     const bool inwin = l < 63 && cur.o < C;  // read rs0+l starts in [P, C)
     const int nst = __popcll(ballot(inwin));
     // ---- per-read slots ----
     if (inwin) {
       const int q = l + 1;
-      const int64_t up = uo_nx - cur.uo, dn = dno_nx - cur.dno;
+      const bool up = uo_nx != cur.uo, dn = dno_nx != cur.dno;  // flank lengths < 2^32
       const int ts = cur.ts;
       uint32_t derr = 0;
       if (ts < 0) derr |= DE_INDEX;                   // deviation: no negative wrap
-      if (up > 0 && ts > n) derr |= DE_INDEX;         // leftIndel(2*i) past the end
+      if (up && ts > n) derr |= DE_INDEX;             // leftIndel(2*i) past the end
       if (o_nx <= cur.o) derr |= DE_OP;               // processOperation('', '')
       if (derr) flag_read(a, derr, rs0 + l);
-      if (up > 0 && ts >= 0 && ts <= n) atomicOr(hl + (ts >> 5), 1u << (ts & 31));  // upstream flank: LEFT at gap tstart
+      if (up && ts >= 0 && ts <= n) atomicOr(hl + (ts >> 5), 1u << (ts & 31));  // upstream flank: LEFT at gap tstart
       W.s_end[q] = o_nx;
       W.s_ts[q] = ts < 0 ? -1 : (ts > kICap ? kICap : ts);
       W.s_read[q] = (int32_t)(rs0 + l);
-      W.s_iend[q] = (ts < 0 ? 0 : (ts > n ? n + 1 : ts)) | (dn > 0 ? 1 << 30 : 0);
+      W.s_iend[q] = (ts < 0 ? 0 : (ts > n ? n + 1 : ts)) | (dn ? 1 << 30 : 0);
     }
     PROF_T(tw1);
     // ---- prefetch the next window ----
@@ -516,34 +566,34 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       int tlo = (int)(P - cA), thi = (int)(C - cA);
       tlo = tlo < 0 ? 0 : (tlo > CH ? CH : tlo);
       thi = thi < 0 ? 0 : (thi > CH ? CH : thi);
-      const uint32_t tm = em_own & ((1u << thi) - 1u) & ~((1u << tlo) - 1u);
+      const uint32_t rng = lowmask(thi) & ~lowmask(tlo);
+      const uint32_t tm = em_own & rng;
       // Units: a ':' token with 1-4 operand bytes and the op token ('*', '+',
       // '-') right after it in the same read, both in [P, C), are ONE list
       // entry (bits 12-14: the ':' operand length); every other token is its
-      // own entry.  Bit-parallel over this lane's bytes and its neighbours'
-      // (DPP wave shifts): bit CH + k of a 3-lane mask = own byte k.
-      uint32_t cm_own, om_own;
-      class_masks(cur.d, &cm_own, &om_own);
-      const uint32_t rng = ((1u << thi) - 1u) & ~((1u << tlo) - 1u);
+      // own entry.  Bit-parallel over this lane's bytes and the 5 bytes either
+      // side (DPP wave shifts): bit 5 + k of a neighbourhood mask = own byte k.
       const uint32_t cmr = cm_own & rng, omr = om_own & ~ra_own & rng;
-      const uint64_t em3 = (uint64_t)from_lane_below(em_own) | ((uint64_t)em_own << CH) |
-                           ((uint64_t)from_lane_above(em_own) << (2 * CH));
-      const uint64_t cm3 = (uint64_t)from_lane_below(cmr) | ((uint64_t)cmr << CH) |
-                           ((uint64_t)from_lane_above(cmr) << (2 * CH));
-      const uint64_t om3 = ((uint64_t)omr << CH) | ((uint64_t)from_lane_above(omr) << (2 * CH));
+      auto hood = [&](uint32_t x, bool below, bool above) {
+        uint64_t h = (uint64_t)x << 5;
+        if (below) h |= (uint64_t)((from_lane_below(x) >> (CH - 5)) & 31u);
+        if (above) h |= (uint64_t)(from_lane_above(x) & 31u) << (CH + 5);
+        return h;
+      };
+      const uint64_t em3 = hood(em_own, true, true), cm3 = hood(cmr, true, true), om3 = hood(omr, false, true);
       const uint64_t nb1 = ~(em3 << 1), nb12 = nb1 & ~(em3 << 2), nb123 = nb12 & ~(em3 << 3);
       const uint64_t c2 = (cm3 << 2) & nb1;                   // ':' 2 bytes before, no boundary between
       const uint64_t c3 = (cm3 << 3) & nb12;
       const uint64_t c4 = (cm3 << 4) & nb123;
       const uint64_t c5 = (cm3 << 5) & nb123 & ~(em3 << 4);
       const uint64_t ab = om3 & (c2 | c3 | c4 | c5);          // absorbed ops
-      const uint32_t own = CH == 16 ? 0xffffu : 0xffu;
-      const uint32_t p2 = (uint32_t)(((ab & c2) >> (CH + 2))) & own;  // ':' whose op is 2 bytes on
-      const uint32_t p3 = (uint32_t)(((ab & c3) >> (CH + 3))) & own;
-      const uint32_t p4 = (uint32_t)(((ab & c4) >> (CH + 4))) & own;
-      const uint32_t p5 = (uint32_t)(((ab & c5) >> (CH + 5))) & own;
+      const uint32_t own = lowmask(CH);
+      const uint32_t p2 = (uint32_t)((ab & c2) >> 7) & own;  // ':' whose op is 2 bytes on
+      const uint32_t p3 = (uint32_t)((ab & c3) >> 8) & own;
+      const uint32_t p4 = (uint32_t)((ab & c4) >> 9) & own;
+      const uint32_t p5 = (uint32_t)((ab & c5) >> 10) & own;
       const uint32_t pl0 = p2 | p4, pl1 = p3 | p4;            // operand length d - 1 in 3 bit planes
-      const uint32_t tu = tm & ~((uint32_t)(ab >> CH) & own);
+      const uint32_t tu = tm & ~((uint32_t)(ab >> 5) & own);
       const int cnt = __popc(tu);
       const int incl = wave_scan_i32(cnt);
       T = wave_last_i32(incl);
@@ -564,6 +614,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     // ---- rounds: one token per lane ----
     int32_t G = 0;  // advances of the window's earlier rounds
     int qc = 0;     // read starts of the window's earlier rounds
+#ifdef MPC_EXP_NOROUNDS
+    T = 0;  // timing experiment: window overhead only (results invalid)
+#endif
     for (int t0 = 0; t0 < T; t0 += 64) {
       const int t = t0 + l;
       const bool v = t < T;
@@ -595,14 +648,22 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const bool act = v & spec & ((olen > 0) | last);  // empty operand: skipped unless last (:309, :320)
       const int ol4 = olen < 0 ? 0 : (olen > 4 ? 4 : olen);
       const uint32_t vm = ol4 == 4 ? 0xffffffffu : ((1u << (8 * ol4)) - 1u);  // operand bytes in w0
-      //   ':' up to 4 digits -> right-align, SWAR decimal conversion (pairs, quad)
-      const uint32_t Tx = w0 ^ 0x30303030u;
-      const uint32_t nd = (((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u;
-      const bool dig_ok = (olen >= 1) & (olen <= 4) & ((nd & vm) == 0);
-      uint32_t X = (Tx & vm & 0x0F0F0F0Fu) << (8 * (4 - ol4));
+      //   the unit's ':' operand -- its prefix (pl bytes after s0) or the main
+      //   token's own operand -- up to 4 digits: right-align, SWAR decimal
+      const bool pre = pl != 0;
+      const int pa = (s0 + 1) >> 2;
+      const uint32_t pw = __builtin_amdgcn_alignbyte(b32[pa + 1], b32[pa], (uint32_t)((s0 + 1) & 3));
+      const int cl = pre ? pl : (colon ? ol4 : 0);
+      const uint32_t cw = pre ? pw : w0;
+      const uint32_t cvm = cl == 4 ? 0xffffffffu : ((1u << (8 * cl)) - 1u);
+      const uint32_t Tx = cw ^ 0x30303030u;
+      const bool cdig = ((((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u & cvm) == 0;
+      uint32_t X = cl == 0 ? 0u : (Tx & cvm & 0x0F0F0F0Fu) << (8 * (4 - cl));
       X = mul2561(X) >> 8;
       X = ((X & 0x00FF00FFu) * 6553601u) >> 16;
       const int adv_c = (int)(X & 0xffffu);
+      int adv0 = pre ? adv_c : 0;
+      const bool dig_ok = (olen >= 1) & (olen <= 4) & cdig;  // main ':' token
       //   bases: (c|0x20) must equal "acgt"[h] with h = (lc>>1)&3 (v_perm table lookup)
       const uint32_t lc = w0 | 0x20202020u;
       const uint32_t hh = (lc >> 1) & 0x03030303u;
@@ -614,17 +675,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       pk = (pk | (pk >> 6)) & 0x000f000fu;
       pk = (pk | (pk >> 12)) & 0xffu;
       uint32_t pay = star ? ((codes >> shl) & 3u) : (pk & ((1u << (2 * ol4)) - 1u));
-      //   prefix ':' operand (pl bytes after s0)
-      const int pa = (s0 + 1) >> 2;
-      const uint32_t pw = __builtin_amdgcn_alignbyte(b32[pa + 1], b32[pa], (uint32_t)((s0 + 1) & 3));
-      const uint32_t pvm = pl == 0 ? 0u : pl == 4 ? 0xffffffffu : ((1u << (8 * pl)) - 1u);
-      const uint32_t pT = pw ^ 0x30303030u;
-      const uint32_t pnd = (((pT & 0x7F7F7F7Fu) + 0x76767676u) | pT) & 0x80808080u;
-      uint32_t pX = pl == 0 ? 0u : (pT & pvm & 0x0F0F0F0Fu) << (8 * (4 - pl));
-      pX = mul2561(pX) >> 8;
-      pX = ((pX & 0x00FF00FFu) * 6553601u) >> 16;
-      int adv0 = (int)(pX & 0xffffu);
-      const bool slow = lfar | (v & ((pnd & pvm) != 0)) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));
+      const bool slow = lfar | (pre & !cdig) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));
       int kind = !act ? 0 : colon ? (adv_c > 0 ? 1 : 0) : (olen <= 0) ? 0 : star ? 2 : plus ? 3 : minus ? 4 : 0;
       int adv = kind == 1 ? adv_c : kind == 2 ? 1 : kind == 4 ? (olen < kAdvCap ? olen : kAdvCap) : 0;
       uint32_t err = (v & !spec) ? DE_OP : 0u;  // cs does not start with an operator (:100-102)
@@ -1955,6 +2006,7 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
 
 static const void* parse_kernel(bool fused, int win) {
   if (win == 512) return fused ? (const void*)K_parse<true, 512> : (const void*)K_parse<false, 512>;
+  if (win == 2048) return fused ? (const void*)K_parse<true, 2048> : (const void*)K_parse<false, 2048>;
   return fused ? (const void*)K_parse<true, 1024> : (const void*)K_parse<false, 1024>;
 }
 static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
@@ -1963,6 +2015,9 @@ static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
   if (p->parse_win == 512) {
     if (p->fused) hipLaunchKernelGGL((K_parse<true, 512>), g, b, p->parse_lds, st, a);
     else hipLaunchKernelGGL((K_parse<false, 512>), g, b, p->parse_lds, st, a);
+  } else if (p->parse_win == 2048) {
+    if (p->fused) hipLaunchKernelGGL((K_parse<true, 2048>), g, b, p->parse_lds, st, a);
+    else hipLaunchKernelGGL((K_parse<false, 2048>), g, b, p->parse_lds, st, a);
   } else {
     if (p->fused) hipLaunchKernelGGL((K_parse<true, 1024>), g, b, p->parse_lds, st, a);
     else hipLaunchKernelGGL((K_parse<false, 1024>), g, b, p->parse_lds, st, a);
@@ -2109,12 +2164,13 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     const int lds_cap = 160 * 1024;
     const int max_waves_cu = 16;  // VGPR budget of K_parse (~106 VGPRs -> 4 waves per SIMD)
     auto lds_of = [&](int win, bool fu, int nw) {
-      return win == 512 ? parse_lds_bytes<512>((int)n_max, fu, p->nbmax, nw)
-                        : parse_lds_bytes<1024>((int)n_max, fu, p->nbmax, nw);
+      return win == 512    ? parse_lds_bytes<512>((int)n_max, fu, p->nbmax, nw)
+             : win == 2048 ? parse_lds_bytes<2048>((int)n_max, fu, p->nbmax, nw)
+                           : parse_lds_bytes<1024>((int)n_max, fu, p->nbmax, nw);
     };
     int best = -1, per_cu = 1;
     for (int fu = 1; fu >= 0 && best < 0; --fu)
-      for (int win : {1024, 512})
+      for (int win : {2048, 1024, 512})
         for (int nw : {16, 12, 8}) {
           const int lds = lds_of(win, fu != 0, nw);
           if (lds > lds_cap) continue;
@@ -2126,7 +2182,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     p->parse_lds = lds_of(p->parse_win, p->fused, p->parse_nw);
     if (const char* e = getenv("MPC_PARSE_GEOM")) {  // experiments: "win,nw"
       int wv = 0, nv = 0;
-      if (sscanf(e, "%d,%d", &wv, &nv) == 2 && (wv == 512 || wv == 1024) && nv >= 1 && nv <= kMaxPW &&
+      if (sscanf(e, "%d,%d", &wv, &nv) == 2 && (wv == 512 || wv == 1024 || wv == 2048) && nv >= 1 && nv <= kMaxPW &&
           lds_of(wv, p->fused, nv) <= lds_cap) {
         p->parse_win = wv; p->parse_nw = nv; p->parse_lds = lds_of(wv, p->fused, nv);
         per_cu = std::max(1, std::min(lds_cap / p->parse_lds, 32 / nv));

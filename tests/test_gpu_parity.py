@@ -160,3 +160,54 @@ def test_sharded_matches_oracle(pkg, spec, n_shards):
         for k, plan in enumerate(sp.plans):
             for s, (r, e) in enumerate(zip(plan.fetch(), exp)):
                 _cmp(r, e, ("shard", k, s, mdf))
+
+
+def _packed(ref, css, tstarts, flank_seed=0):
+    """A sample dict (synth layout) from explicit cs strings."""
+    rng = np.random.default_rng(flank_seed)
+    cs_b = [c.encode() for c in css]
+    acgt = np.frombuffer(b"ACGT", dtype=np.uint8)
+    ups = [rng.choice(acgt, int(rng.integers(0, 6))).tobytes() for _ in css]
+    dns = [rng.choice(acgt, int(rng.integers(0, 6))).tobytes() for _ in css]
+    off = lambda xs: np.concatenate([[0], np.cumsum([len(x) for x in xs])]).astype(np.int64)
+    arr = lambda xs: np.frombuffer(b"".join(xs) or b"", dtype=np.uint8).copy()
+    return dict(ref=np.frombuffer(ref, dtype=np.uint8).copy(), cs=arr(cs_b), cs_off=off(cs_b),
+                tstart=np.asarray(tstarts, dtype=np.int64), up=arr(ups), up_off=off(ups), down=arr(dns),
+                down_off=off(dns))
+
+
+def _dense_cs(rng, n, ts):
+    """Valid cs made of 1-3 byte tokens (empty ':' operands are skipped by the
+    reference unless last): up to one boundary per byte, so 2 KiB windows hit
+    their unit cap, and ':'+op pairs sit at every distance and lane seam."""
+    out, i = ["Z:"], ts
+    stop = int(rng.integers(n // 2, n - 3))
+    while True:
+        r = rng.random()
+        if r < 0.25:
+            out.append(":")
+        elif r < 0.45 and i < n - 1:
+            k = int(rng.integers(1, 3))
+            out.append(":%d" % k); i += k
+        elif r < 0.6:
+            out.append("+" + "".join(rng.choice(list("acgtACGT"), int(rng.integers(1, 3)))))
+        elif r < 0.75 and i < n - 2:
+            out.append("-" + "".join(rng.choice(list("acgt"), 1))); i += 1
+        elif r < 0.9 and i < n - 1:
+            out.append("*a" + str(rng.choice(list("cgtCGT")))); i += 1
+        if i >= stop:
+            out.append(":1")
+            return "".join(out)
+
+
+@pytest.mark.parametrize("seed", [1, 2])
+def test_dense_tokens_match_oracle(pkg, seed):
+    rng = np.random.default_rng(seed)
+    n = 3000
+    ref = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), n).tobytes()
+    ts = [int(rng.integers(0, 40)) for _ in range(300)]
+    css = [_dense_cs(rng, n, t) for t in ts]
+    smp = _packed(ref, css, ts, seed)
+    assert max(np.diff(smp["cs_off"])) > 2048  # reads span several windows
+    for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
+        _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("dense", seed, mdf))

@@ -145,9 +145,9 @@ int mpc_plan_set_input(mpc_plan* plan, const mpc_input* in);
  *   mpc_rows     ; SUM ROWS  (odd rows come from shard 0, others add flank / insertion bases)
  *   mpc_consensus (identical on every shard) */
 int mpc_parse(mpc_plan* plan, void* stream);        /* clear; cs -> i_end, LEFT gap bits, tallies, insertion events */
-int mpc_index(mpc_plan* plan, void* stream);        /* downstream (RIGHT) events at mixed gaps, stable (gap, read) sort */
+int mpc_index(mpc_plan* plan, void* stream);        /* downstream (RIGHT) events at mixed gaps, stable (gap, read) sort; insertion work units */
 int mpc_runs(mpc_plan* plan, void* stream);         /* shards > 1: global run index space            */
-int mpc_tally(mpc_plan* plan, void* stream);        /* work units; longest LEFT string per run (M)   */
+int mpc_tally(mpc_plan* plan, void* stream);        /* longest LEFT string per run (M)               */
 int mpc_layout(mpc_plan* plan, void* stream);       /* per-gap replay of the slot layout, row counts */
 int mpc_rows(mpc_plan* plan, void* stream);         /* row offsets, depth, odd rows, insertion and flank tallies */
 int mpc_consensus(mpc_plan* plan, double min_depth_factor, double global_threshold_factor,

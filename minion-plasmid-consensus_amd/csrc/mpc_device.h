@@ -77,6 +77,16 @@ __device__ __forceinline__ int wave_scan_i32(int x) {
   x += dpp_i32<0x143, 0xc>(x);   // row_bcast:31 -> rows 2, 3
   return x;
 }
+// inclusive max-scan for x >= 0 (lanes outside a row / broadcast read 0)
+__device__ __forceinline__ int wave_scan_max_i32(int x) {
+  x = max(x, dpp_i32<0x111>(x));
+  x = max(x, dpp_i32<0x112>(x));
+  x = max(x, dpp_i32<0x114>(x));
+  x = max(x, dpp_i32<0x118>(x));
+  x = max(x, dpp_i32<0x142, 0xa>(x));
+  x = max(x, dpp_i32<0x143, 0xc>(x));
+  return x;
+}
 __device__ __forceinline__ int wave_last_i32(int x) { return __builtin_amdgcn_readlane(x, 63); }
 __device__ __forceinline__ int uniform_i32(int x) { return __builtin_amdgcn_readfirstlane(x); }
 

@@ -632,6 +632,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const bool last = v && (e1 >> 15);
       const uint64_t brs = ballot(is_rs);
       const int q = qc + lanes_below(brs) + (is_rs ? 1 : 0);
+      // the read's slot, loaded before the decode (a read starting in this
+      // round needs no s_val: see the coordinates below)
+      const int32_t q_val = W.s_val[q], q_ts = W.s_ts[q], q_read = W.s_read[q], q_iend = W.s_iend[q];
       // fast decode from the staged bytes: op, then 4 operand bytes
       const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage);
       const int a4 = sx >> 2;
@@ -699,9 +702,12 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const int ainc = wave_scan_i32(advu);
       const int aex = ainc - advu;
       const int atot = wave_last_i32(ainc);
-      if (is_rs) W.s_val[q] = W.s_ts[q] - (G + aex);
-      wave_sync_lds();
-      const int iu = W.s_val[q] + G + aex;    // coordinate at the unit start
+      // a read starting in this round (rs lane j <= l): i = tstart + the
+      // advances since lane j = aex - aex(j); aex never decreases, so aex(j)
+      // is a max-scan over the rs lanes (DPP: no LDS round trip)
+      const int aex_rs = wave_scan_max_i32(is_rs ? aex : 0);
+      if (is_rs) W.s_val[q] = q_ts - (G + aex);  // for later rounds and the window carry
+      const int iu = q > qc ? q_ts + (aex - aex_rs) : q_val + G + aex;  // coordinate at the unit start
       const int i = iu + adv0;                // ... and at its main token
       // ---- effects ----
       uint32_t te = err;
@@ -709,7 +715,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if (kind == 1 && (i < 0 || i + adv > n)) te |= DE_INDEX;
       if (kind == 2 && (uint32_t)i >= (uint32_t)n) te |= DE_INDEX;
       if (kind == 3 && (uint32_t)i > (uint32_t)n) te |= DE_INDEX;
-      const int rl = W.s_read[q];
+      const int rl = q_read;
       if (te == 0) {
         if (kind == 2) odd_sub(i, (int)pay);
         if (kind == 4 && i >= 0 && i < n) {
@@ -727,10 +733,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if (last) {  // the read's last operation: i_end, downstream check, span
         const int ia = i + adv;
         const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
-        const int dnf = W.s_iend[q] & (1 << 30);
+        const int dnf = q_iend & (1 << 30);
         if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
         W.s_iend[q] = ie | dnf;
-        const int ts = W.s_ts[q];
+        const int ts = q_ts;
         const int e2 = ie > n ? n : ie;
         if (ts >= 0 && ts < e2) { depth_inc(ts); depth_dec(e2); }
       }
@@ -779,16 +785,19 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   __syncthreads();
   // ---- flush LDS tallies and the LEFT-gap bitmap ----
   if (fused) {
+    // one word per lane, consecutive lanes on consecutive words: a wave's
+    // atomics cover contiguous bytes (memory-side atomics run at full rate
+    // only on contiguous segments)
     for (int p = threadIdx.x; p <= n; p += blockDim.x) {
       const uint32_t dl = del_l[p];
       const int32_t dv = (int32_t)(dl >> 16) - (int32_t)(dl & 0xffffu);
       if (dv) atomicAdd(a.diff + gb + p, dv);
-      const uint32_t s0 = sub_l[2 * p], s1 = sub_l[2 * p + 1];
-      uint32_t* sg = a.sub + (int64_t)(gb + p) * 4;
-      if (s0 & 0xffffu) atomicAdd(sg + 0, s0 & 0xffffu);
-      if (s0 >> 16) atomicAdd(sg + 1, s0 >> 16);
-      if (s1 & 0xffffu) atomicAdd(sg + 2, s1 & 0xffffu);
-      if (s1 >> 16) atomicAdd(sg + 3, s1 >> 16);
+    }
+    uint32_t* sg = a.sub + (int64_t)gb * 4;
+    for (int k = threadIdx.x; k < 4 * (n + 1); k += blockDim.x) {  // word k = position k/4, code k%4
+      const uint32_t w2 = sub_l[2 * (k >> 2) + ((k >> 1) & 1)];
+      const uint32_t v = (k & 1) ? (w2 >> 16) : (w2 & 0xffffu);
+      if (v) atomicAdd(sg + k, v);
     }
   }
   for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) {
@@ -1957,6 +1966,7 @@ struct mpc_plan {
   Dev dev() const;
 };
 
+
 template <class T>
 static T* at(const mpc_plan* p, int b) { return reinterpret_cast<T*>(p->ws + p->off[b]); }
 
@@ -2376,6 +2386,9 @@ int mpc_index(mpc_plan* p, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
   const int32_t nrb = (int32_t)((p->N + kRS - 1) / kRS);
+  // (the insertion work units need only the parse; one stream: a second one's
+  // event fork/join cost more than the overlap gained, measured)
+  if (p->n_bc > 0) hipLaunchKernelGGL(K_units, dim3(nblk(p->n_bc, 4)), dim3(256), 0, st, unit_args(p, d));
   if (p->N > 0) hipLaunchKernelGGL(K_rsplit, dim3(nrb), dim3(kRS), 0, st, d);
   hipLaunchKernelGGL(K_rsort, dim3(1), dim3(kRS), 0, st, d, nrb, (int32_t)p->end_bit);
   hipLaunchKernelGGL(K_rstart, dim3(nblk(std::max<int64_t>(p->G + 1, p->N))), dim3(256), 0, st, d);  // (M <= N)
@@ -2399,8 +2412,7 @@ int mpc_tally(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  if (p->n_bc > 0) hipLaunchKernelGGL(K_units, dim3(nblk(p->n_bc, 4)), dim3(256), 0, st, unit_args(p, d));
-  hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));
+  hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));  // (units: mpc_index)
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }

@@ -4,23 +4,23 @@
 // reference function to its replacement; DESIGN.md has layouts and rooflines).
 //
 // Pipeline (one stream, no host synchronization):
-//   parse     K_parse       per workgroup: contiguous reads of one sample.  cs
-//                           tokens -> substitution / deletion / span tallies
-//                           (LDS), insertion events (bucket-sorted by gap),
-//                           i_end, LEFT-event gap bitmap, data-error flags
-//   index     K_rsplit      downstream (RIGHT) events: mixed gaps -> sort keys,
-//                           RIGHT-only gaps -> longest flank
-//             radix sort    stable (gap, read) order of mixed RIGHT events
-//             K_rstart      per-gap ranges in the sorted list
-//   tally     K_left        one workgroup per 16-gap bucket: insertion tallies F
-//                           and max LEFT length M per run; upstream flank M
-//   layout    K_seg*,K_replay  per-gap replay of the slot-layout state of
-//                           processBaseString_* (:37-72), row offsets (scan)
-//   rows      scan          depth = prefix(difference array)
-//             K_assemble    odd rows + F -> rows (plain stores)
-//             K_flank       flanks (per gap bucket, dense LDS rows) + long insertions
-//   consensus K_call        per-slot top/second/tie/N (:363-439), max depth
-//             scan, K_emit  threshold test + ordered compaction of the calls
+//   parse     K_clear        zero the per-launch state
+//             K_parse        per workgroup: contiguous reads of one sample.  cs
+//                            ':'+op units -> substitution / deletion / span
+//                            tallies (LDS), insertion events (bucket-sorted by
+//                            gap), i_end, LEFT-event gap bitmap, error flags
+//   index     K_rsplit_units RIGHT events: mixed gaps -> sort keys, RIGHT-only
+//                            gaps -> longest flank; insertion work units
+//             K_rsort        stable (gap, read) order of the mixed RIGHT events
+//             K_rstart       per-gap ranges in the sorted list, RIGHT run lengths
+//   runs      K_runs, K_runR (several shards) global run index space
+//   tally     K_left         longest LEFT string per run (insertions, upstream flanks)
+//   layout    K_replay       per-gap replay of the slot-layout state of
+//                            processBaseString_* (:37-72) -> row counts
+//   rows      K_assemble     row offsets + depth (block prefixes), odd rows
+//             K_ins, K_flank insertion / flank bases onto their slot rows
+//   consensus K_call         per-slot top/second/tie/N (:363-439), max depth
+//             K_keep, K_emit threshold test + ordered compaction of the calls
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
@@ -863,11 +863,11 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool has_left(const uint32_t* bm, int64_t g) { return (bm[g >> 5] >> (g & 31)) & 1u; }
 
-__global__ __launch_bounds__(1024) void K_rsplit(Dev d) {
+__device__ __forceinline__ void rsplit_block(const Dev& d, int64_t b) {
   __shared__ int64_t s_key;
   __shared__ int32_t s_val;
   __shared__ int32_t s_w[16];
-  const int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  const int64_t r = b * blockDim.x + threadIdx.x;
   const bool in = r < d.N;
   int64_t g = -1;
   int32_t len = 0;
@@ -894,11 +894,11 @@ __global__ __launch_bounds__(1024) void K_rsplit(Dev d) {
   int wpre = 0;
   for (int k = 0; k < w; ++k) wpre += s_w[k];
   if (mixed) {
-    const int64_t o = (int64_t)blockIdx.x * blockDim.x + wpre + inc - 1;
+    const int64_t o = b * blockDim.x + wpre + inc - 1;
     d.keys_in[o] = (uint32_t)g;
     d.vals_in[o] = (int32_t)rg;
   }
-  if (threadIdx.x == blockDim.x - 1) d.bcnt[blockIdx.x] = wpre + inc;
+  if (threadIdx.x == blockDim.x - 1) d.bcnt[b] = wpre + inc;
   block_atomic_max(d.maxR, g < 0 ? 0 : g, len, in && g >= 0 && !mixed, &s_key, &s_val);
 }
 
@@ -1113,9 +1113,8 @@ struct UnitArgs {
 };
 
 // one wave per table entry
-__global__ __launch_bounds__(256) void K_units(UnitArgs a) {
+__device__ __forceinline__ void units_entry(const UnitArgs& a, int64_t ent) {
   const int l = lane();
-  const int64_t ent = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
   if (ent >= a.n_bc) return;
   const int4 bc = a.bc[ent];
   int t = 0;
@@ -1134,6 +1133,14 @@ __global__ __launch_bounds__(256) void K_units(UnitArgs a) {
     const int e0 = i * kUnit;
     a.units[u0 + i] = make_int4((int)ent, e0, t - e0 < kUnit ? t - e0 : kUnit, 0);
   }
+}
+
+// One launch for two independent jobs after the parse: blocks [0, nrb) split
+// the RIGHT events (one read per thread), the rest cut the insertion work
+// units (one table entry per wave).  Block-uniform branch.
+__global__ __launch_bounds__(kRS) void K_rsplit_units(Dev d, UnitArgs ua, int32_t nrb) {
+  if ((int32_t)blockIdx.x < nrb) rsplit_block(d, blockIdx.x);
+  else units_entry(ua, ((int64_t)blockIdx.x - nrb) * (kRS / 64) + (threadIdx.x >> 6));
 }
 
 // Per unit: the entry's <= 256 slices (counts, sources) lane-parallel, block
@@ -2386,10 +2393,10 @@ int mpc_index(mpc_plan* p, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
   const int32_t nrb = (int32_t)((p->N + kRS - 1) / kRS);
-  // (the insertion work units need only the parse; one stream: a second one's
-  // event fork/join cost more than the overlap gained, measured)
-  if (p->n_bc > 0) hipLaunchKernelGGL(K_units, dim3(nblk(p->n_bc, 4)), dim3(256), 0, st, unit_args(p, d));
-  if (p->N > 0) hipLaunchKernelGGL(K_rsplit, dim3(nrb), dim3(kRS), 0, st, d);
+  // the insertion work units need only the parse: cut in the RIGHT-split launch
+  // (one stream: a second one's event fork/join cost more than the overlap, measured)
+  const int32_t nub = (int32_t)((p->n_bc + kRS / 64 - 1) / (kRS / 64));  // unit-cutting blocks
+  if (nrb + nub > 0) hipLaunchKernelGGL(K_rsplit_units, dim3(nrb + nub), dim3(kRS), 0, st, d, unit_args(p, d), nrb);
   hipLaunchKernelGGL(K_rsort, dim3(1), dim3(kRS), 0, st, d, nrb, (int32_t)p->end_bit);
   hipLaunchKernelGGL(K_rstart, dim3(nblk(std::max<int64_t>(p->G + 1, p->N))), dim3(256), 0, st, d);  // (M <= N)
   HIPCHK(hipGetLastError());

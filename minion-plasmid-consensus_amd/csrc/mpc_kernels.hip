@@ -1264,7 +1264,10 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
     __syncthreads();
   }
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
-  const int64_t tid = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  // the per-read parts start at the first block that had no unit (rotated
+  // block index), so they run beside the unit blocks instead of after them
+  const int64_t fb = ((int64_t)blockIdx.x + gridDim.x - nunits % gridDim.x) % gridDim.x;
+  const int64_t tid = fb * blockDim.x + threadIdx.x;
   // long insertions
   const int64_t nov = *a.ovf_cnt < (uint32_t)a.ovf_cap ? *a.ovf_cnt : a.ovf_cap;
   for (int64_t t = tid; t < nov; t += nthreads) {
@@ -1273,7 +1276,7 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
     atomicMax(a.M + run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + o.read), o.len);
   }
   // upstream flanks (block-uniform trips: block_atomic_max synchronizes the block)
-  for (int64_t r0 = (int64_t)blockIdx.x * blockDim.x; r0 < a.N; r0 += nthreads) {
+  for (int64_t r0 = fb * blockDim.x; r0 < a.N; r0 += nthreads) {
     const int64_t r = r0 + threadIdx.x;
     int64_t run = 0;
     int32_t L = 0;
@@ -1517,9 +1520,11 @@ __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
       }
     __syncthreads();
   }
-  // long insertions (grid-stride, LEFT like the short ones)
+  // long insertions (grid-stride, LEFT like the short ones; from the first
+  // block that had no unit, so they run beside the unit blocks)
   const int64_t nov = *a.ovf_cnt < (uint32_t)a.ovf_cap ? *a.ovf_cnt : a.ovf_cap;
-  for (int64_t t = (int64_t)blockIdx.x * (kUB / 64) + w; t < nov; t += (int64_t)gridDim.x * (kUB / 64)) {
+  const int64_t fb = ((int64_t)blockIdx.x + gridDim.x - nunits % gridDim.x) % gridDim.x;
+  for (int64_t t = fb * (kUB / 64) + w; t < nov; t += (int64_t)gridDim.x * (kUB / 64)) {
     const Ovf o = a.ovf[t];
     const int64_t g = a.gbase[a.sample[o.read]] + o.gap;
     const int64_t run = run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + o.read);

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MPC_ABI_VERSION 3
+#define MPC_ABI_VERSION 4
 
 /* return codes */
 #define MPC_OK 0
@@ -112,11 +112,11 @@ enum {
   MPC_BUF_RIGHT_CNT,    /* int32[gaps] this shard's mixed RIGHT events per gap     (exchange: all-gather) */
   MPC_BUF_RIGHT_CNT_ALL,/* int32[n_shards][gaps] all shards' MPC_BUF_RIGHT_CNT   (exchange: target)     */
   MPC_BUF_HASLEFT,      /* uint32[(gaps+31)/32 + 1] bitmap: gap holds a LEFT event (exchange: OR)         */
-  MPC_BUF_MAXR,         /* int32[gaps] longest RIGHT event at RIGHT-only gaps       (exchange: MAX)        */
-  MPC_BUF_RUN_M,        /* int32[n_reads_global + gaps] longest LEFT event per run  (exchange: MAX)        */
-  MPC_BUF_RUN_R,        /* int32[n_reads_global + gaps] length of the RIGHT event closing each run (exchange: MAX) */
-  MPC_BUF_DIFF,         /* int32[gaps] read-span/deletion difference array          (exchange: SUM)        */
-  MPC_BUF_SUB,          /* uint32[gaps][4] substitution tallies                     (exchange: SUM)        */
+  MPC_BUF_MAXR,         /* int32[gaps] longest RIGHT event at RIGHT-only gaps       (exchange: MAX, span)  */
+  MPC_BUF_RUN_M,        /* int32[n_reads_global + gaps] longest LEFT event per run  (exchange: MAX, span)  */
+  MPC_BUF_RUN_R,        /* int32[n_reads_global + gaps] length of the RIGHT event closing each run (MAX, span) */
+  MPC_BUF_DIFF,         /* int32[gaps] this shard's read-span/deletion difference array (not exchanged)    */
+  MPC_BUF_SUB,          /* uint32[gaps][4] this shard's substitution tallies        (not exchanged)        */
   MPC_BUF_COUNT
 };
 
@@ -137,12 +137,14 @@ int mpc_plan_set_input(mpc_plan* plan, const mpc_input* in);
 
 /* Phases (single GPU: mpc_run() = all of them, in this order).  With
  * n_shards > 1 the host inserts these collectives (Multi-GPU):
- *   mpc_parse    ; OR  HASLEFT, SUM DIFF/SUB (may be deferred to before layout)
- *   mpc_index    ; ALL-GATHER RIGHT_CNT -> RIGHT_CNT_ALL, MAX MAXR
+ *   mpc_parse    ; OR  HASLEFT
+ *   mpc_index    ; ALL-GATHER RIGHT_CNT -> RIGHT_CNT_ALL
  *   mpc_runs     (global run index space, RIGHT length per run)
- *   mpc_tally    ; MAX RUN_M, MAX RUN_R
+ *   mpc_tally    ; MAX over the span MAXR .. RUN_R (MAXR, RUN_M, RUN_R lie in this order
+ *                  in the workspace, with padding between them: one collective)
  *   mpc_layout   (identical on every shard)
- *   mpc_rows     ; SUM ROWS  (odd rows come from shard 0, others add flank / insertion bases)
+ *   mpc_rows     ; SUM ROWS  (every shard's rows hold its own reads' counts, odd
+ *                  positions included: DIFF / SUB are never exchanged)
  *   mpc_consensus (identical on every shard) */
 int mpc_parse(mpc_plan* plan, void* stream);        /* clear; cs -> i_end, LEFT gap bits, tallies, insertion events */
 int mpc_index(mpc_plan* plan, void* stream);        /* downstream (RIGHT) events at mixed gaps, stable (gap, read) sort; insertion work units */

@@ -1418,7 +1418,7 @@ __global__ __launch_bounds__(kGB) void K_assemble(Dev d) {
   if (nslots > 0) d.meta[rb] = 2;  // first slot of the gap
   if (p < n) {
     uint4 out = make_uint4(0, 0, 0, 0);
-    if (d.shard == 0) {  // rows are summed over shards: odd rows come from shard 0
+    {  // each shard: its own reads' depth and substitutions (rows are summed over shards)
       // odd position p: depth = reads covering p with a match or substitution
       const uint32_t* sb = d.sub + g * 4;
       const uint32_t s0 = sb[0], s1 = sb[1], s2 = sb[2], s3 = sb[3];
@@ -1967,8 +1967,9 @@ struct mpc_plan {
   bool fused = false;
   enum {
     B_STATUS, B_NOF, B_GBASE, B_IEND, B_INSRAW, B_INSSORT, B_BKCNT, B_BKOFF, B_RBASE, B_OVF, B_OVFCNT,
-    B_HASLEFT, B_MAXR, B_KIN, B_VIN, B_KOUT, B_VOUT, B_KTMP, B_VTMP, B_BCNT, B_BPRE, B_RLEN, B_RPOS, B_RSTART, B_RSLOC, B_ROFF, B_RCNT, B_RCNTALL,
-    B_DIFF, B_SUB, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
+    B_HASLEFT, B_KIN, B_VIN, B_KOUT, B_VOUT, B_KTMP, B_VTMP, B_BCNT, B_BPRE, B_RLEN, B_RPOS, B_RSTART, B_RSLOC, B_ROFF, B_RCNT, B_RCNTALL,
+    // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
+    B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
     B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_COUNT
   };
   size_t off[B_COUNT];

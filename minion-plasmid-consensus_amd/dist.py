@@ -154,15 +154,12 @@ def exchange_step(plans, ex, mdf, gtf, stream=None):
 
     each("parse")
     ex.reduce([p.buffer(eng.BUF_HASLEFT, i32) for p in plans], "or")
-    ex.reduce([p.buffer(eng.BUF_DIFF, i32) for p in plans], "sum")
-    ex.reduce([p.buffer(eng.BUF_SUB, i32) for p in plans], "sum")
     each("index")
     ex.gather([p.buffer(eng.BUF_RIGHT_CNT, i32) for p in plans], [p.buffer(eng.BUF_RIGHT_CNT_ALL, i32) for p in plans])
-    ex.reduce([p.buffer(eng.BUF_MAXR, i32) for p in plans], "max")
     each("runs")
     each("tally")
-    ex.reduce([p.buffer(eng.BUF_RUN_M, i32) for p in plans], "max")
-    ex.reduce([p.buffer(eng.BUF_RUN_R, i32) for p in plans], "max")
+    # MAXR (RIGHT-only gaps), RUN_M, RUN_R: adjacent in the workspace, one MAX
+    ex.reduce([p.span(eng.BUF_MAXR, eng.BUF_RUN_R, i32) for p in plans], "max")
     each("layout")
     each("rows")
     ex.reduce([p.buffer(eng.BUF_ROWS, i32) for p in plans], "sum")

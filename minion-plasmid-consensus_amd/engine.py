@@ -14,7 +14,7 @@ from . import _build
 
 LIB_PATH = os.environ.get("MPC_LIB", _build.LIBMPC)  # override: experiments with library variants
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED = 0, 1, 2, 3
 DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL = 1, 2, 4, 8, 16, 32
 (BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_CNT, BUF_RIGHT_CNT_ALL,
@@ -220,6 +220,19 @@ class Plan:
         _check(lib().mpc_plan_buffer(self.h, which, ctypes.byref(off), ctypes.byref(cnt)))
         item = torch.empty(0, dtype=dtype).element_size()
         return self.ws[off.value: off.value + cnt.value * item].view(dtype)
+
+    def span(self, first, last, dtype):
+        """The workspace bytes from buffer ``first`` through buffer ``last``
+        (include/mpc.h: buffers exchanged together are laid out in order)."""
+        torch = _torch()
+        o0, c0, o1, c1 = ctypes.c_size_t(), ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_int64()
+        _check(lib().mpc_plan_buffer(self.h, first, ctypes.byref(o0), ctypes.byref(c0)))
+        _check(lib().mpc_plan_buffer(self.h, last, ctypes.byref(o1), ctypes.byref(c1)))
+        item = torch.empty(0, dtype=dtype).element_size()
+        end = o1.value + c1.value * item
+        if o1.value < o0.value or (end - o0.value) % item:
+            raise MpcError("buffers %d..%d are not an ordered span" % (first, last))
+        return self.ws[o0.value: end].view(dtype)
 
     def stream_ptr(self, stream=None):
         torch = _torch()

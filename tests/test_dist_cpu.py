@@ -33,11 +33,14 @@ class FakePlan:
         _, eng = _mod()
         rng = np.random.default_rng(1000 + shard)
         i = lambda *shape, hi=1000: torch.from_numpy(rng.integers(0, hi, size=shape).astype(np.int32))
+        # MAXR, RUN_M, RUN_R: one workspace span with padding between them (include/mpc.h)
+        self.mx = i(G + 5 + (G + 11) + 3 + (G + 11))
+        a, b = G + 5, 2 * G + 16 + 3
         self.buf = {
             eng.BUF_HASLEFT: i((G + 31) // 32 + 1, hi=2 ** 30),
             eng.BUF_DIFF: i(G), eng.BUF_SUB: i(4 * G),
             eng.BUF_RIGHT_CNT: i(G, hi=50), eng.BUF_RIGHT_CNT_ALL: torch.zeros(n_shards * G, dtype=torch.int32),
-            eng.BUF_MAXR: i(G), eng.BUF_RUN_M: i(G + 11), eng.BUF_RUN_R: i(G + 11),
+            eng.BUF_MAXR: self.mx[:G], eng.BUF_RUN_M: self.mx[a:a + G + 11], eng.BUF_RUN_R: self.mx[b:b + G + 11],
             eng.BUF_ROWS: i(4 * ROWS),
         }
         self.initial = {k: v.clone() for k, v in self.buf.items()}
@@ -49,14 +52,20 @@ class FakePlan:
     def buffer(self, which, dtype):
         return self.buf[which]
 
+    def span(self, first, last, dtype):
+        _, eng = _mod()
+        assert (first, last) == (eng.BUF_MAXR, eng.BUF_RUN_R)
+        return self.mx
+
 
 def expected(n_shards):
     _, eng = _mod()
     plans = [FakePlan(k, n_shards) for k in range(n_shards)]
     init = [p.initial for p in plans]
     out = {}
-    for b, op in ((eng.BUF_HASLEFT, "or"), (eng.BUF_DIFF, "sum"), (eng.BUF_SUB, "sum"), (eng.BUF_MAXR, "max"),
-                  (eng.BUF_RUN_M, "max"), (eng.BUF_RUN_R, "max"), (eng.BUF_ROWS, "sum")):
+    # DIFF / SUB stay per shard (every shard's rows carry its own odd-position counts)
+    for b, op in ((eng.BUF_HASLEFT, "or"), (eng.BUF_MAXR, "max"), (eng.BUF_RUN_M, "max"), (eng.BUF_RUN_R, "max"),
+                  (eng.BUF_ROWS, "sum")):
         acc = init[0][b].clone()
         for x in init[1:]:
             acc = acc + x[b] if op == "sum" else (acc.maximum(x[b]) if op == "max" else acc | x[b])
@@ -78,7 +87,8 @@ def test_local_exchange_combines():
         assert p.log[-1] == ("consensus", 0.1, 5.0)
         for b, v in exp.items():
             assert torch.equal(p.buf[b], v), b
-        assert torch.equal(p.buf[eng.BUF_RIGHT_CNT], p.initial[eng.BUF_RIGHT_CNT])  # own counts untouched
+        for b in (eng.BUF_RIGHT_CNT, eng.BUF_DIFF, eng.BUF_SUB):  # per-shard buffers untouched
+            assert torch.equal(p.buf[b], p.initial[b]), b
 
 
 def test_shard_layout_and_split():

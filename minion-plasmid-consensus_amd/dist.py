@@ -78,25 +78,29 @@ class DistExchange:
         elif op == "max":
             d.all_reduce(t, op=d.ReduceOp.MAX, group=self.group)
         elif op == "or":
-            # RCCL has no bitwise reduction: gather the bitmaps and OR them
-            import torch
-            parts = [torch.empty_like(t) for _ in range(self.world)]
-            d.all_gather(parts, t, group=self.group)
-            acc = parts[0].clone()
-            for x in parts[1:]:
-                acc |= x
-            t.copy_(acc)
+            # RCCL has no bitwise reduction: gather the bitmaps, OR them as a tree
+            st = self._gather_rows(t)
+            k = self.world
+            while k > 1:
+                h = (k + 1) // 2  # rows [h, k) fold onto [0, k - h)
+                st[: k - h] |= st[h:k]
+                k = h
+            t.copy_(st[0])
         else:
             raise ValueError(op)
 
+    def _gather_rows(self, t, out=None):
+        """(world, len(t)) tensor of every rank's t, by one all_gather_into_tensor
+        (straight into ``out`` when given; RCCL and gloo alike)."""
+        import torch
+        if out is None:
+            out = torch.empty((self.world,) + tuple(t.shape), dtype=t.dtype, device=t.device)
+        self.dist.all_gather_into_tensor(out.view(-1), t.contiguous(), group=self.group)
+        return out
+
     def gather(self, ts, outs):
         (t,), (o,) = ts, outs
-        import torch
-        parts = list(o.view(self.world, -1).unbind(0))
-        tmp = [torch.empty_like(t) for _ in range(self.world)]
-        self.dist.all_gather(tmp, t, group=self.group)
-        for p, x in zip(parts, tmp):
-            p.copy_(x)
+        self._gather_rows(t, o.view(self.world, -1))
 
     def _ints(self, xs, op):
         import torch

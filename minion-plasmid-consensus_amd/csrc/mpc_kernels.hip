@@ -188,8 +188,12 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
 __host__ __device__ inline int parse_hl_words(int n) { return (n + 1 + 31) / 32; }
 __host__ __device__ constexpr int parse_misc_bytes() { return kMaxPW * 4 + kMaxPW * 8; }
 template <int WIN>
-__host__ __device__ inline int parse_lds_bytes(int n_max, bool fused, int nbmax, int nw) {
-  const int tallies = fused ? 12 * (n_max + 1) : 0;  // sub 4 x u16, deletion/span starts | ends u16
+// position tallies of K_parse: 0 = global atomics, 1 = LDS, 12 B per position
+// (sub 4 x u16, depth decrements | increments u16), 2 = LDS, 10 B per position
+// (the depth difference as one biased 16-bit half): fits 2 KiB windows beside
+// ~10 kb references
+__host__ __device__ inline int parse_lds_bytes(int n_max, int tm, int nbmax, int nw) {
+  const int tallies = tm == 0 ? 0 : tm == 1 ? 12 * (n_max + 1) : 8 * (n_max + 1) + 4 * ((n_max + 2) / 2);
   const int buckets = 8 * nbmax + 4 * (kMaxPW + 2);  // counts + cursors + per-wave prefix
   return nw * (int)sizeof(WaveLds<WIN>) + parse_misc_bytes() + 4 * parse_hl_words(n_max) +
          (tallies > buckets ? tallies : buckets);
@@ -400,7 +404,7 @@ __device__ unsigned long long g_prof[16];
 #define PROF_ADD(k, v)
 #endif
 
-template <bool FUSED, int WIN>
+template <int TM, int WIN>
 __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   constexpr int CH = WIN / 64;
   using WL = WaveLds<WIN>;
@@ -423,11 +427,17 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int gb = a.gbase[smp];
   uint32_t* uni = hl + parse_hl_words(n);
   uint32_t* sub_l = uni;                // [2 (n+1)]: A | T << 16, C | G << 16
-  uint32_t* del_l = uni + 2 * (n + 1);  // [n+1]: depth-decrement count | depth-increment count << 16
-  constexpr bool fused = FUSED;         // tallies in LDS (one address space per instantiation)
+  // TM 1: [n+1] depth-decrement count | depth-increment count << 16
+  // TM 2: [(n+2)/2] depth difference of position p in half p&1 of word p>>1,
+  //       biased by 0x8000: at most 16383 reads per workgroup and 2 per read and
+  //       position keep every partial sum inside (0, 0xffff): no carry across halves
+  uint32_t* del_l = uni + 2 * (n + 1);
+  constexpr bool fused = TM != 0;       // tallies in LDS (one address space per instantiation)
+  constexpr bool packed = TM == 2;
   for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) hl[k] = 0;
   if (fused)
-    for (int k = threadIdx.x; k < 3 * (n + 1); k += blockDim.x) uni[k] = 0;
+    for (int k = threadIdx.x; k < 2 * (n + 1) + (packed ? (n + 2) / 2 : n + 1); k += blockDim.x)
+      uni[k] = (packed && k >= 2 * (n + 1)) ? 0x80008000u : 0u;
   __syncthreads();
 
   auto odd_sub = [&](int pos, int code) {
@@ -435,11 +445,13 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     else atomicAdd(a.sub + (int64_t)(gb + pos) * 4 + code, 1u);
   };
   auto depth_dec = [&](int pos) {  // diff[pos] -= 1
-    if (fused) atomicAdd(del_l + pos, 1u);
+    if (packed) atomicSub(del_l + (pos >> 1), 1u << (16 * (pos & 1)));
+    else if (fused) atomicAdd(del_l + pos, 1u);
     else atomicAdd(a.diff + gb + pos, -1);
   };
   auto depth_inc = [&](int pos) {  // diff[pos] += 1
-    if (fused) atomicAdd(del_l + pos, 1u << 16);
+    if (packed) atomicAdd(del_l + (pos >> 1), 1u << (16 * (pos & 1)));
+    else if (fused) atomicAdd(del_l + pos, 1u << 16);
     else atomicAdd(a.diff + gb + pos, 1);
   };
 
@@ -789,8 +801,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     // atomics cover contiguous bytes (memory-side atomics run at full rate
     // only on contiguous segments)
     for (int p = threadIdx.x; p <= n; p += blockDim.x) {
-      const uint32_t dl = del_l[p];
-      const int32_t dv = (int32_t)(dl >> 16) - (int32_t)(dl & 0xffffu);
+      int32_t dv;
+      if (packed) dv = (int32_t)((del_l[p >> 1] >> (16 * (p & 1))) & 0xffffu) - 0x8000;
+      else { const uint32_t dl = del_l[p]; dv = (int32_t)(dl >> 16) - (int32_t)(dl & 0xffffu); }
       if (dv) atomicAdd(a.diff + gb + p, dv);
     }
     uint32_t* sg = a.sub + (int64_t)gb * 4;
@@ -1964,7 +1977,7 @@ struct mpc_plan {
   int n_parse_wg = 0, parse_lds = 0, nbmax = 1, parse_win = 1024, parse_nw = 8;
   int64_t n_bc = 0, units_cap = 0;
   int32_t shard = 0, n_shards = 1;
-  bool fused = false;
+  int tally_mode = 0;  // K_parse TM
   enum {
     B_STATUS, B_NOF, B_GBASE, B_IEND, B_INSRAW, B_INSSORT, B_BKCNT, B_BKOFF, B_RBASE, B_OVF, B_OVFCNT,
     B_HASLEFT, B_KIN, B_VIN, B_KOUT, B_VOUT, B_KTMP, B_VTMP, B_BCNT, B_BPRE, B_RLEN, B_RPOS, B_RSTART, B_RSLOC, B_ROFF, B_RCNT, B_RCNTALL,
@@ -2027,24 +2040,25 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   return a;
 }
 
-static const void* parse_kernel(bool fused, int win) {
-  if (win == 512) return fused ? (const void*)K_parse<true, 512> : (const void*)K_parse<false, 512>;
-  if (win == 2048) return fused ? (const void*)K_parse<true, 2048> : (const void*)K_parse<false, 2048>;
-  return fused ? (const void*)K_parse<true, 1024> : (const void*)K_parse<false, 1024>;
+// instantiated (tally mode, window) pairs; packed tallies only with 1 and 2 KiB windows
+static const void* parse_kernel(int tm, int win) {
+  if (tm == 2) return win == 1024 ? (const void*)K_parse<2, 1024> : (const void*)K_parse<2, 2048>;
+  if (win == 512) return tm ? (const void*)K_parse<1, 512> : (const void*)K_parse<0, 512>;
+  if (win == 2048) return tm ? (const void*)K_parse<1, 2048> : (const void*)K_parse<0, 2048>;
+  return tm ? (const void*)K_parse<1, 1024> : (const void*)K_parse<0, 1024>;
 }
 static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
   const dim3 g(p->n_parse_wg), b(p->parse_nw * 64);
   const ParseArgs a = parse_args(p, d);
-  if (p->parse_win == 512) {
-    if (p->fused) hipLaunchKernelGGL((K_parse<true, 512>), g, b, p->parse_lds, st, a);
-    else hipLaunchKernelGGL((K_parse<false, 512>), g, b, p->parse_lds, st, a);
-  } else if (p->parse_win == 2048) {
-    if (p->fused) hipLaunchKernelGGL((K_parse<true, 2048>), g, b, p->parse_lds, st, a);
-    else hipLaunchKernelGGL((K_parse<false, 2048>), g, b, p->parse_lds, st, a);
-  } else {
-    if (p->fused) hipLaunchKernelGGL((K_parse<true, 1024>), g, b, p->parse_lds, st, a);
-    else hipLaunchKernelGGL((K_parse<false, 1024>), g, b, p->parse_lds, st, a);
-  }
+  const int tm = p->tally_mode, win = p->parse_win;
+  if (tm == 2 && win == 1024) hipLaunchKernelGGL((K_parse<2, 1024>), g, b, p->parse_lds, st, a);
+  else if (tm == 2) hipLaunchKernelGGL((K_parse<2, 2048>), g, b, p->parse_lds, st, a);
+  else if (win == 512 && tm) hipLaunchKernelGGL((K_parse<1, 512>), g, b, p->parse_lds, st, a);
+  else if (win == 512) hipLaunchKernelGGL((K_parse<0, 512>), g, b, p->parse_lds, st, a);
+  else if (win == 2048 && tm) hipLaunchKernelGGL((K_parse<1, 2048>), g, b, p->parse_lds, st, a);
+  else if (win == 2048) hipLaunchKernelGGL((K_parse<0, 2048>), g, b, p->parse_lds, st, a);
+  else if (tm) hipLaunchKernelGGL((K_parse<1, 1024>), g, b, p->parse_lds, st, a);
+  else hipLaunchKernelGGL((K_parse<0, 1024>), g, b, p->parse_lds, st, a);
 }
 
 static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
@@ -2182,32 +2196,39 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       n_max = std::max<int64_t>(n_max, p->ref_len[s]);
       p->nbmax = std::max<int>(p->nbmax, (int)((p->ref_len[s] + 1 + kBW - 1) / kBW));
     }
-    // parse geometry: window size and waves per workgroup that give the most
-    // resident waves per CU with the position tallies in LDS (12 B per position)
+    // parse geometry: tally mode, window and waves per workgroup that give the
+    // most resident waves per CU (ties: the earlier candidate -- LDS tallies,
+    // larger windows, the 12-byte tallies)
     const int lds_cap = 160 * 1024;
-    const int max_waves_cu = 16;  // VGPR budget of K_parse (~106 VGPRs -> 4 waves per SIMD)
-    auto lds_of = [&](int win, bool fu, int nw) {
-      return win == 512    ? parse_lds_bytes<512>((int)n_max, fu, p->nbmax, nw)
-             : win == 2048 ? parse_lds_bytes<2048>((int)n_max, fu, p->nbmax, nw)
-                           : parse_lds_bytes<1024>((int)n_max, fu, p->nbmax, nw);
+    const int max_waves_cu = 16;  // VGPR budget of K_parse (<= 128 VGPRs -> 4 waves per SIMD)
+    auto lds_of = [&](int win, int tm, int nw) {
+      return win == 512    ? parse_lds_bytes<512>((int)n_max, tm, p->nbmax, nw)
+             : win == 2048 ? parse_lds_bytes<2048>((int)n_max, tm, p->nbmax, nw)
+                           : parse_lds_bytes<1024>((int)n_max, tm, p->nbmax, nw);
     };
+    // score = resident waves x window efficiency (measured at C2: 512 B windows
+    // cost ~25 % more per byte than 2 KiB ones, 1 KiB ~5 %)
+    static const int cand[8][2] = {{1, 2048}, {2, 2048}, {1, 1024}, {2, 1024}, {1, 512}, {0, 2048}, {0, 1024}, {0, 512}};
     int best = -1, per_cu = 1;
-    for (int fu = 1; fu >= 0 && best < 0; --fu)
-      for (int win : {2048, 1024, 512})
-        for (int nw : {16, 12, 8}) {
-          const int lds = lds_of(win, fu != 0, nw);
-          if (lds > lds_cap) continue;
-          const int wgs = std::max(1, std::min(lds_cap / lds, max_waves_cu / nw));
-          const int waves = wgs * nw;
-          if (waves > best) { best = waves; p->fused = fu != 0; p->parse_win = win; p->parse_nw = nw; per_cu = wgs; }
-        }
+    for (const auto& c : cand)  // global-atomic tallies (tm 0) only when no LDS mode fits
+      for (int nw : {16, 12, 8}) {
+        if (c[0] == 0 && best > 0) break;
+        const int lds = lds_of(c[1], c[0], nw);
+        if (lds > lds_cap) continue;
+        const int wgs = std::max(1, std::min(lds_cap / lds, max_waves_cu / nw));
+        const int score = wgs * nw * (c[1] == 512 ? 75 : c[1] == 1024 ? 95 : 100);
+        if (score > best) { best = score; p->tally_mode = c[0]; p->parse_win = c[1]; p->parse_nw = nw; per_cu = wgs; }
+      }
     if (best < 0) { delete p; return fail(MPC_E_ARG, "reference too long for the LDS budget"); }
-    p->parse_lds = lds_of(p->parse_win, p->fused, p->parse_nw);
+    p->parse_lds = lds_of(p->parse_win, p->tally_mode, p->parse_nw);
+    if (getenv("MPC_DEBUG_GEOM"))
+      fprintf(stderr, "K_parse geometry: tally mode %d, window %d, %d waves, %d B LDS\n", p->tally_mode, p->parse_win,
+              p->parse_nw, p->parse_lds);
     if (const char* e = getenv("MPC_PARSE_GEOM")) {  // experiments: "win,nw"
       int wv = 0, nv = 0;
       if (sscanf(e, "%d,%d", &wv, &nv) == 2 && (wv == 512 || wv == 1024 || wv == 2048) && nv >= 1 && nv <= kMaxPW &&
-          lds_of(wv, p->fused, nv) <= lds_cap) {
-        p->parse_win = wv; p->parse_nw = nv; p->parse_lds = lds_of(wv, p->fused, nv);
+          (p->tally_mode != 2 || wv != 512) && lds_of(wv, p->tally_mode, nv) <= lds_cap) {
+        p->parse_win = wv; p->parse_nw = nv; p->parse_lds = lds_of(wv, p->tally_mode, nv);
         per_cu = std::max(1, std::min(lds_cap / p->parse_lds, 32 / nv));
       }
     }
@@ -2219,7 +2240,8 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       if (ns <= 0) continue;
       int64_t ch = std::max<int64_t>(1, (target * ns + std::max<int64_t>(p->N, 1) - 1) / std::max<int64_t>(p->N, 1));
       ch = std::min<int64_t>(ch, (ns + 63) / 64);
-      ch = std::max<int64_t>(ch, (ns + 32766) / 32767);  // LDS tallies are 16-bit (<= 2 per read and position)
+      const int64_t wg_reads = p->tally_mode == 2 ? 16383 : 32767;  // 16-bit LDS tallies (<= 2 per read and position)
+      ch = std::max<int64_t>(ch, (ns + wg_reads - 1) / wg_reads);
       for (int64_t c = 0; c < ch; ++c) {
         const int64_t x = a + ns * c / ch, y = a + ns * (c + 1) / ch;
         if (y > x) p->work_parse.insert(p->work_parse.end(), {s, (int32_t)x, (int32_t)y, 0});
@@ -2331,7 +2353,7 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WPARSE), p->work_parse.data(), 4 * p->work_parse.size(), hipMemcpyHostToDevice));
   if (!p->work_bc.empty())
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WBC), p->work_bc.data(), 4 * p->work_bc.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipFuncSetAttribute(parse_kernel(p->fused, p->parse_win), hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
+  HIPCHK(hipFuncSetAttribute(parse_kernel(p->tally_mode, p->parse_win), hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
   p->bound = true;
   return MPC_OK;
 }

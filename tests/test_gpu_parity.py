@@ -93,6 +93,10 @@ SYNTH = [
     dict(n=50, n_reads=2000, profile="c1probe", seed=7, frac_partial=0.5, flank=(0, 8)),
     dict(n=3000, n_reads=500, profile="default", seed=9, frac_partial=0.3, ins_len=(1, 1500), del_len=(1, 1200),
          p_ins=0.0005, p_del=0.0005, flank=(0, 3000)),
+    # K_parse geometry by reference length: ~10 kb -> packed 10-byte LDS tallies
+    # (tally mode 2), ~20 kb -> global-atomic tallies (mode 0)
+    dict(n=10000, n_reads=1200, profile="indel", seed=44, frac_partial=0.2),
+    dict(n=20000, n_reads=300, profile="default", seed=45, frac_partial=0.3),
 ]
 
 

@@ -190,10 +190,11 @@ __host__ __device__ constexpr int parse_misc_bytes() { return kMaxPW * 4 + kMaxP
 template <int WIN>
 // position tallies of K_parse: 0 = global atomics, 1 = LDS, 12 B per position
 // (sub 4 x u16, depth decrements | increments u16), 2 = LDS, 10 B per position
-// (the depth difference as one biased 16-bit half): fits 2 KiB windows beside
-// ~10 kb references
+// (the depth difference as one biased 16-bit half), 3 = depth differences in
+// LDS (2 B per position), substitutions global: references up to ~40 kb
 __host__ __device__ inline int parse_lds_bytes(int n_max, int tm, int nbmax, int nw) {
-  const int tallies = tm == 0 ? 0 : tm == 1 ? 12 * (n_max + 1) : 8 * (n_max + 1) + 4 * ((n_max + 2) / 2);
+  const int tallies = tm == 0 ? 0 : tm == 1 ? 12 * (n_max + 1) : tm == 2 ? 8 * (n_max + 1) + 4 * ((n_max + 2) / 2)
+                                                                 : 4 * ((n_max + 2) / 2);
   const int buckets = 8 * nbmax + 4 * (kMaxPW + 2);  // counts + cursors + per-wave prefix
   return nw * (int)sizeof(WaveLds<WIN>) + parse_misc_bytes() + 4 * parse_hl_words(n_max) +
          (tallies > buckets ? tallies : buckets);
@@ -426,22 +427,24 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int n = a.n_of[smp];
   const int gb = a.gbase[smp];
   uint32_t* uni = hl + parse_hl_words(n);
-  uint32_t* sub_l = uni;                // [2 (n+1)]: A | T << 16, C | G << 16
-  // TM 1: [n+1] depth-decrement count | depth-increment count << 16
-  // TM 2: [(n+2)/2] depth difference of position p in half p&1 of word p>>1,
-  //       biased by 0x8000: at most 16383 reads per workgroup and 2 per read and
-  //       position keep every partial sum inside (0, 0xffff): no carry across halves
-  uint32_t* del_l = uni + 2 * (n + 1);
-  constexpr bool fused = TM != 0;       // tallies in LDS (one address space per instantiation)
-  constexpr bool packed = TM == 2;
+  constexpr bool fused = TM != 0;           // depth differences in LDS (one address space per instantiation)
+  constexpr bool lds_sub = TM == 1 || TM == 2;  // substitution tallies in LDS too
+  constexpr bool packed = TM >= 2;
+  const int nsub = lds_sub ? 2 * (n + 1) : 0;
+  uint32_t* sub_l = uni;                    // [2 (n+1)] (TM 1, 2): A | T << 16, C | G << 16
+  // TM 1:    [n+1] depth-decrement count | depth-increment count << 16
+  // TM 2, 3: [(n+2)/2] depth difference of position p in half p&1 of word p>>1,
+  //          biased by 0x8000: at most 16383 reads per workgroup and 2 per read and
+  //          position keep every partial sum inside (0, 0xffff): no carry across halves
+  uint32_t* del_l = uni + nsub;
   for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) hl[k] = 0;
   if (fused)
-    for (int k = threadIdx.x; k < 2 * (n + 1) + (packed ? (n + 2) / 2 : n + 1); k += blockDim.x)
-      uni[k] = (packed && k >= 2 * (n + 1)) ? 0x80008000u : 0u;
+    for (int k = threadIdx.x; k < nsub + (packed ? (n + 2) / 2 : n + 1); k += blockDim.x)
+      uni[k] = (packed && k >= nsub) ? 0x80008000u : 0u;
   __syncthreads();
 
   auto odd_sub = [&](int pos, int code) {
-    if (fused) atomicAdd(sub_l + 2 * pos + (code >> 1), 1u << (16 * (code & 1)));
+    if (lds_sub) atomicAdd(sub_l + 2 * pos + (code >> 1), 1u << (16 * (code & 1)));
     else atomicAdd(a.sub + (int64_t)(gb + pos) * 4 + code, 1u);
   };
   auto depth_dec = [&](int pos) {  // diff[pos] -= 1
@@ -807,7 +810,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if (dv) atomicAdd(a.diff + gb + p, dv);
     }
     uint32_t* sg = a.sub + (int64_t)gb * 4;
-    for (int k = threadIdx.x; k < 4 * (n + 1); k += blockDim.x) {  // word k = position k/4, code k%4
+    for (int k = threadIdx.x; lds_sub && k < 4 * (n + 1); k += blockDim.x) {  // word k = position k/4, code k%4
       const uint32_t w2 = sub_l[2 * (k >> 2) + ((k >> 1) & 1)];
       const uint32_t v = (k & 1) ? (w2 >> 16) : (w2 & 0xffffu);
       if (v) atomicAdd(sg + k, v);
@@ -2040,9 +2043,10 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   return a;
 }
 
-// instantiated (tally mode, window) pairs; packed tallies only with 1 and 2 KiB windows
+// instantiated (tally mode, window) pairs; packed modes only with 1 and 2 KiB windows
 static const void* parse_kernel(int tm, int win) {
   if (tm == 2) return win == 1024 ? (const void*)K_parse<2, 1024> : (const void*)K_parse<2, 2048>;
+  if (tm == 3) return win == 1024 ? (const void*)K_parse<3, 1024> : (const void*)K_parse<3, 2048>;
   if (win == 512) return tm ? (const void*)K_parse<1, 512> : (const void*)K_parse<0, 512>;
   if (win == 2048) return tm ? (const void*)K_parse<1, 2048> : (const void*)K_parse<0, 2048>;
   return tm ? (const void*)K_parse<1, 1024> : (const void*)K_parse<0, 1024>;
@@ -2053,6 +2057,8 @@ static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
   const int tm = p->tally_mode, win = p->parse_win;
   if (tm == 2 && win == 1024) hipLaunchKernelGGL((K_parse<2, 1024>), g, b, p->parse_lds, st, a);
   else if (tm == 2) hipLaunchKernelGGL((K_parse<2, 2048>), g, b, p->parse_lds, st, a);
+  else if (tm == 3 && win == 1024) hipLaunchKernelGGL((K_parse<3, 1024>), g, b, p->parse_lds, st, a);
+  else if (tm == 3) hipLaunchKernelGGL((K_parse<3, 2048>), g, b, p->parse_lds, st, a);
   else if (win == 512 && tm) hipLaunchKernelGGL((K_parse<1, 512>), g, b, p->parse_lds, st, a);
   else if (win == 512) hipLaunchKernelGGL((K_parse<0, 512>), g, b, p->parse_lds, st, a);
   else if (win == 2048 && tm) hipLaunchKernelGGL((K_parse<1, 2048>), g, b, p->parse_lds, st, a);
@@ -2207,12 +2213,15 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
                            : parse_lds_bytes<1024>((int)n_max, tm, p->nbmax, nw);
     };
     // score = resident waves x window efficiency (measured at C2: 512 B windows
-    // cost ~25 % more per byte than 2 KiB ones, 1 KiB ~5 %)
-    static const int cand[8][2] = {{1, 2048}, {2, 2048}, {1, 1024}, {2, 1024}, {1, 512}, {0, 2048}, {0, 1024}, {0, 512}};
+    // cost ~25 % more per byte than 2 KiB ones, 1 KiB ~5 %).  Global substitution
+    // atomics (tm 3) lost to tm 2 with fewer waves at C3 (711 vs 491 us) though
+    // they won at C4 (3769 vs 4614 us): tm 3 only when tm 1 / 2 do not fit.
+    static const int cand[10][2] = {{1, 2048}, {2, 2048}, {1, 1024}, {2, 1024}, {1, 512},
+                                    {3, 2048}, {3, 1024}, {0, 2048}, {0, 1024}, {0, 512}};
     int best = -1, per_cu = 1;
-    for (const auto& c : cand)  // global-atomic tallies (tm 0) only when no LDS mode fits
+    for (const auto& c : cand)  // tm 3 only when neither 1 nor 2 fits, tm 0 only when no LDS mode fits
       for (int nw : {16, 12, 8}) {
-        if (c[0] == 0 && best > 0) break;
+        if ((c[0] == 0 || c[0] == 3) && best > 0 && (c[0] == 0 || p->tally_mode != 3)) break;
         const int lds = lds_of(c[1], c[0], nw);
         if (lds > lds_cap) continue;
         const int wgs = std::max(1, std::min(lds_cap / lds, max_waves_cu / nw));
@@ -2227,7 +2236,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     if (const char* e = getenv("MPC_PARSE_GEOM")) {  // experiments: "win,nw"
       int wv = 0, nv = 0;
       if (sscanf(e, "%d,%d", &wv, &nv) == 2 && (wv == 512 || wv == 1024 || wv == 2048) && nv >= 1 && nv <= kMaxPW &&
-          (p->tally_mode != 2 || wv != 512) && lds_of(wv, p->tally_mode, nv) <= lds_cap) {
+          (p->tally_mode < 2 || wv != 512) && lds_of(wv, p->tally_mode, nv) <= lds_cap) {
         p->parse_win = wv; p->parse_nw = nv; p->parse_lds = lds_of(wv, p->tally_mode, nv);
         per_cu = std::max(1, std::min(lds_cap / p->parse_lds, 32 / nv));
       }
@@ -2240,7 +2249,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       if (ns <= 0) continue;
       int64_t ch = std::max<int64_t>(1, (target * ns + std::max<int64_t>(p->N, 1) - 1) / std::max<int64_t>(p->N, 1));
       ch = std::min<int64_t>(ch, (ns + 63) / 64);
-      const int64_t wg_reads = p->tally_mode == 2 ? 16383 : 32767;  // 16-bit LDS tallies (<= 2 per read and position)
+      const int64_t wg_reads = p->tally_mode >= 2 ? 16383 : 32767;  // 16-bit LDS tallies (<= 2 per read and position)
       ch = std::max<int64_t>(ch, (ns + wg_reads - 1) / wg_reads);
       for (int64_t c = 0; c < ch; ++c) {
         const int64_t x = a + ns * c / ch, y = a + ns * (c + 1) / ch;

@@ -94,9 +94,11 @@ SYNTH = [
     dict(n=3000, n_reads=500, profile="default", seed=9, frac_partial=0.3, ins_len=(1, 1500), del_len=(1, 1200),
          p_ins=0.0005, p_del=0.0005, flank=(0, 3000)),
     # K_parse geometry by reference length: ~10 kb -> packed 10-byte LDS tallies
-    # (tally mode 2), ~20 kb -> global-atomic tallies (mode 0)
+    # (tally mode 2), ~20 kb -> LDS depth + global substitutions (mode 3),
+    # ~70 kb -> global-atomic tallies (mode 0)
     dict(n=10000, n_reads=1200, profile="indel", seed=44, frac_partial=0.2),
     dict(n=20000, n_reads=300, profile="default", seed=45, frac_partial=0.3),
+    dict(n=70000, n_reads=60, profile="default", seed=46, frac_partial=0.3),
 ]
 
 

@@ -1717,41 +1717,20 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
         if (tid < nwd) wpre[tid] = p2 + i2 - cnt;
       }
       __syncthreads();
-#ifdef MPC_EXP_NOBYTES_FLANK
-      for (int x0 = 4 * tid; x0 < 0; x0 += 4 * blockDim.x) {
-#else
-      for (int x0 = 4 * tid; x0 < cn; x0 += 4 * blockDim.x) {
-#endif
-        const uint32_t* b32 = reinterpret_cast<const uint32_t*>(stage);
-        const int sx = x0 + sh0;
-        const uint32_t v = __builtin_amdgcn_alignbyte(b32[(sx >> 2) + 1], b32[sx >> 2], (uint32_t)(sx & 3));
-        const uint32_t word = bm[x0 >> 5];
-        const int bpos = x0 & 31;
-        int cur = wpre[x0 >> 5] + __popc(word & ((bpos == 0) ? 0u : ((1u << bpos) - 1u)));  // starts before x0
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int x = x0 + k;
-          if (x >= cn) break;
-          cur += (word >> (bpos + k)) & 1u;
-          const int o = cur;  // owner: index in the compacted list
-          const int32_t rw = t_row[o];
-          if (rw < 0) continue;
-          const int64_t row = (int64_t)rw + (c0 + x - t_start[o]);
-          const int code = code_exact((v >> (8 * k)) & 0xffu);
-          if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
-          const int64_t wr = row - w0;
-#ifdef MPC_EXP_NOATOM_FLANK
-          lread ^= (wr + code);
-          if (true) {} else
-#endif
-          if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 4 + code, 1u);
-          else {
-            atomicAdd(a.rows + row * 4 + code, 1u);
-#ifdef MPC_EXP_COUNT_FLANK
-            atomicAdd(&a.status[6], 1u);
-#endif
-          }
-        }
+      // consecutive lanes take consecutive bytes: a flank's bytes go to
+      // consecutive rows, so a wave's (rare) global atomics cover a few
+      // contiguous segments instead of one scattered row per lane
+      for (int x = tid; x < cn; x += blockDim.x) {
+        const uint32_t word = bm[x >> 5];
+        const int o = wpre[x >> 5] + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
+        const int32_t rw = t_row[o];
+        if (rw < 0) continue;
+        const int64_t row = (int64_t)rw + (c0 + x - t_start[o]);
+        const int code = code_exact(stage[x + sh0]);
+        if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
+        const int64_t wr = row - w0;
+        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 4 + code, 1u);
+        else atomicAdd(a.rows + row * 4 + code, 1u);
       }
     }
   }
@@ -1763,10 +1742,6 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
       if (v) atomicAdd(a.rows + w0 * 4 + k, v);
     }
   }
-#ifdef MPC_EXP_NOATOM_FLANK
-  if (lread == 12345) a.status[7] = 1;
-  lread = INT64_MAX;
-#endif
   if (lerr) {
     atomicOr(&a.status[MPC_ST_FLAGS], lerr);
     if (lread != INT64_MAX) atomicMin(&a.status[MPC_ST_FIRST_READ], (uint32_t)lread);

@@ -1775,7 +1775,8 @@ __device__ __forceinline__ int sample_of_row_lds(const Dev& d, const int32_t* sr
   return lo;
 }
 
-constexpr int kCB = 1024;  // rows per block of the consensus kernels (4 per thread)
+constexpr int kCR = 1;          // rows per thread of K_call (more blocks: the kernel is latency-bound)
+constexpr int kCB = 256 * kCR;  // rows per K_call block
 
 // per slot: sorted(tuples in dict order, key=count)[::-1] -> top / second / tie -> N (:363-423)
 __device__ __forceinline__ uint4 call_slot(uint4 cv, double gtf, uint32_t* total_out) {
@@ -1818,10 +1819,10 @@ __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
     const int64_t rr = threadIdx.x == 0 ? b0 : (b0 + kCB < need ? b0 + kCB : need) - 1;
     s_blk[threadIdx.x] = rr >= 0 ? sample_of_row_lds(d, srow, rr) : 0;
   }
-  uint4 cv[4];
-  uint8_t mt[4];
+  uint4 cv[kCR];
+  uint8_t mt[kCR];
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {  // all loads first
+  for (int k = 0; k < kCR; ++k) {  // all loads first
     const int64_t row = b0 + threadIdx.x + 256 * k;
     cv[k] = row < need ? reinterpret_cast<const uint4*>(d.rows)[row] : make_uint4(0, 0, 0, 0);
     mt[k] = row < need ? d.meta[row] : 0;
@@ -1830,7 +1831,7 @@ __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
   const bool one = s_blk[0] == s_blk[1];
   int32_t mx = -1;
 #pragma unroll
-  for (int k = 0; k < 4; ++k) {
+  for (int k = 0; k < kCR; ++k) {
     const int64_t row = b0 + threadIdx.x + 256 * k;
     uint32_t total = 0;
     const uint4 out = call_slot(cv[k], d.gtf, &total);
@@ -1852,7 +1853,7 @@ __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
 }
 
 // keep[row] = emitted (:428) and per-block counts (kKB rows per block)
-constexpr int kKB = kCB;
+constexpr int kKB = 1024;  // rows per K_keep / K_emit block (4 per thread)
 __global__ __launch_bounds__(256) void K_keep(Dev d, int64_t R) {
   __shared__ int32_t srow[kSmpLds];
   __shared__ int32_t s_w[4];

@@ -206,6 +206,7 @@ class Plan:
         self.ws_raw = torch.empty(self.ws_bytes + 256, dtype=torch.uint8, device=batch.device)
         pad = (-self.ws_raw.data_ptr()) % 256
         self.ws = self.ws_raw[pad: pad + self.ws_bytes]
+        self._views = {}
         _check(L.mpc_plan_bind(h, ctypes.c_void_p(self.ws.data_ptr()), self.ws_bytes))
 
     def __del__(self):
@@ -215,6 +216,14 @@ class Plan:
             self.h = None
 
     def buffer(self, which, dtype):
+        """View of one workspace buffer (memoized: the binding never moves)."""
+        key = ("b", which, dtype)
+        v = self._views.get(key)
+        if v is None:
+            v = self._views[key] = self._buffer(which, dtype)
+        return v
+
+    def _buffer(self, which, dtype):
         torch = _torch()
         off, cnt = ctypes.c_size_t(), ctypes.c_int64()
         _check(lib().mpc_plan_buffer(self.h, which, ctypes.byref(off), ctypes.byref(cnt)))
@@ -224,6 +233,13 @@ class Plan:
     def span(self, first, last, dtype):
         """The workspace bytes from buffer ``first`` through buffer ``last``
         (include/mpc.h: buffers exchanged together are laid out in order)."""
+        key = ("s", first, last, dtype)
+        v = self._views.get(key)
+        if v is None:
+            v = self._views[key] = self._span(first, last, dtype)
+        return v
+
+    def _span(self, first, last, dtype):
         torch = _torch()
         o0, c0, o1, c1 = ctypes.c_size_t(), ctypes.c_int64(), ctypes.c_size_t(), ctypes.c_int64()
         _check(lib().mpc_plan_buffer(self.h, first, ctypes.byref(o0), ctypes.byref(c0)))

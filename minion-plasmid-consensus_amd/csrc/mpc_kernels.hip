@@ -195,7 +195,7 @@ template <int WIN>
 __host__ __device__ inline int parse_lds_bytes(int n_max, int tm, int nbmax, int nw) {
   const int tallies = tm == 0 ? 0 : tm == 1 ? 12 * (n_max + 1) : tm == 2 ? 8 * (n_max + 1) + 4 * ((n_max + 2) / 2)
                                                                  : 4 * ((n_max + 2) / 2);
-  const int buckets = 8 * nbmax + 4 * (kMaxPW + 2);  // counts + cursors + per-wave prefix
+  const int buckets = 16 * nbmax + 4;  // epilogue: counts, cursors, chunk counts, chunk offsets
   return nw * (int)sizeof(WaveLds<WIN>) + parse_misc_bytes() + 4 * parse_hl_words(n_max) +
          (tallies > buckets ? tallies : buckets);
 }
@@ -798,6 +798,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   }
 #endif
   __syncthreads();
+#ifdef MPC_EXP_NOEPI
+  return;  // timing experiment: no flush, no bucket sort (results invalid)
+#endif
   // ---- flush LDS tallies and the LEFT-gap bitmap ----
   if (fused) {
     // one word per lane, consecutive lanes on consecutive words: a wave's
@@ -824,29 +827,37 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     if (g0 & 31) atomicOr(a.hasleft + (g0 >> 5) + 1, v >> (32 - (g0 & 31)));
   }
   __syncthreads();
+#ifdef MPC_EXP_NOSORT
+  return;  // timing experiment: no bucket sort (results invalid)
+#endif
   // ---- bucket-sort this workgroup's insertion events by gap (counting sort) ----
   const int nbk = (n + 1 + kBW - 1) / kBW;
   uint32_t* bcnt = uni;  // aliases the (flushed) tallies
   uint32_t* bcur = bcnt + nbk;
-  int32_t* wpre = reinterpret_cast<int32_t*>(bcur + nbk);  // [kMaxPW + 1]
   for (int k = threadIdx.x; k < nbk; k += blockDim.x) bcnt[k] = 0;
-  if (threadIdx.x == 0) {
-    int s = 0;
-    for (int k = 0; k < nw; ++k) { wpre[k] = s; s += (int)wcnt[k]; }
-    wpre[nw] = s;
-  }
   __syncthreads();
-  const int Ev = wpre[nw];
   const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;
-  auto ev_src = [&](int k) {  // k-th event of the workgroup (wave regions in wave order)
-    int ww = 0;
-    while (ww + 1 < nw && wpre[ww + 1] <= k) ++ww;
-    return wbase[ww] + (k - wpre[ww]);
-  };
-  for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
-    const uint64_t ev = a.ins_raw[ev_src(k)];
-    const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
-    if (gap <= (uint32_t)n) atomicAdd(bcnt + gap / kBW, 1u);
+  // both passes walk the wave regions (wcnt[ww] events at wbase[ww]) in wave
+  // order, coalesced, kEpiB loads in flight per thread
+  constexpr int kEpiB = 4;
+#ifndef MPC_EPIU
+#define MPC_EPIU 8
+#endif
+  constexpr int kEpiU = MPC_EPIU;  // events per thread per staged scatter chunk
+  const int bstride = (int)blockDim.x;
+  for (int ww = 0; ww < nw; ++ww) {
+    const uint64_t* src = a.ins_raw + wbase[ww];
+    const int c = (int)wcnt[ww];
+    for (int k0 = threadIdx.x; k0 < c; k0 += kEpiB * bstride) {
+      uint64_t ev[kEpiB];
+#pragma unroll
+      for (int u = 0; u < kEpiB; ++u) ev[u] = k0 + u * bstride < c ? src[k0 + u * bstride] : ~0ull;
+#pragma unroll
+      for (int u = 0; u < kEpiB; ++u) {
+        const uint32_t gap = (uint32_t)(ev[u] >> 10) & kNullGap;
+        if (gap <= (uint32_t)n) atomicAdd(bcnt + gap / kBW, 1u);
+      }
+    }
   }
   __syncthreads();
   if (threadIdx.x < 64) {  // exclusive scan over buckets by one wave
@@ -865,10 +876,65 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   }
   if (threadIdx.x == 0) a.rbase[blockIdx.x] = rb_wg;
   __syncthreads();
-  for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
-    const uint64_t ev = a.ins_raw[ev_src(k)];
-    const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
-    if (gap <= (uint32_t)n) a.ins_sorted[rb_wg + atomicAdd(bcur + gap / kBW, 1u)] = ev;
+  // scatter, staged: chunks of the workgroup's events (the wave regions
+  // concatenated) are counting-sorted by bucket in LDS (the per-wave areas are
+  // free now), then written out so that consecutive lanes store consecutive
+  // addresses of a bucket's run (8-byte scattered stores left most 128-byte
+  // lines partially written: ~8x HBM write amplification at C4)
+  uint64_t* dst = a.ins_sorted + rb_wg;
+  uint32_t* ccnt = bcur + nbk;  // [nbk] per-chunk bucket counts
+  uint32_t* coff = ccnt + nbk;  // [nbk + 1] their exclusive scan (coff[nbk]: events staged)
+  uint64_t* stg = reinterpret_cast<uint64_t*>(lds);
+  const int chunk = min(nw * (int)sizeof(WL) / 8, kEpiU * bstride);
+  for (int k = threadIdx.x; k < nbk; k += bstride) ccnt[k] = 0;
+  int Ev = 0;
+  for (int ww = 0; ww < nw; ++ww) Ev += (int)wcnt[ww];
+  int ww_t = 0, pre_t = 0;  // this thread's walk over the regions (its k only grow)
+  __syncthreads();
+  for (int c0 = 0; c0 < Ev; c0 += chunk) {
+    const int c1 = min(c0 + chunk, Ev);
+    uint64_t ev[kEpiU];
+    uint32_t rk[kEpiU];
+#pragma unroll
+    for (int u = 0; u < kEpiU; ++u) {
+      const int k = c0 + (int)threadIdx.x + u * bstride;
+      ev[u] = ~0ull;
+      if (k < c1) {
+        while (k >= pre_t + (int)wcnt[ww_t]) { pre_t += (int)wcnt[ww_t]; ++ww_t; }
+        ev[u] = a.ins_raw[wbase[ww_t] + (k - pre_t)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kEpiU; ++u) {
+      const uint32_t gap = (uint32_t)(ev[u] >> 10) & kNullGap;
+      rk[u] = gap <= (uint32_t)n ? atomicAdd(ccnt + gap / kBW, 1u) : ~0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      int cb = 0;
+      for (int b0 = 0; b0 < nbk; b0 += 64) {
+        const int k = b0 + l;
+        const int v = k < nbk ? (int)ccnt[k] : 0;
+        const int inc = wave_scan_i32(v);
+        if (k < nbk) coff[k] = (uint32_t)(cb + inc - v);
+        cb += wave_last_i32(inc);
+      }
+      if (l == 0) coff[nbk] = (uint32_t)cb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kEpiU; ++u)
+      if (rk[u] != ~0u) stg[coff[((uint32_t)(ev[u] >> 10) & kNullGap) / kBW] + rk[u]] = ev[u];
+    __syncthreads();
+    const int staged = (int)coff[nbk];
+    for (int j = threadIdx.x; j < staged; j += bstride) {
+      const uint64_t e = stg[j];
+      const int b = (int)(((uint32_t)(e >> 10) & kNullGap) / kBW);
+      dst[bcur[b] + (j - (int)coff[b])] = e;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nbk; k += bstride) { bcur[k] += ccnt[k]; ccnt[k] = 0; }
+    __syncthreads();
   }
 }
 
@@ -1117,8 +1183,14 @@ __device__ __forceinline__ int64_t run_left(const int32_t* rs, const int32_t* rs
 // K_units cuts every entry's events into units of <= kUnit events (hot
 // buckets become many units) and appends them to one list.
 // ---------------------------------------------------------------------------
-constexpr int kUB = 1024;             // threads of the unit kernels (K_left, K_ins)
-constexpr int kEPT = 8;               // events per thread per unit (loads batched)
+#ifndef MPC_UB
+#define MPC_UB 1024
+#endif
+#ifndef MPC_EPT
+#define MPC_EPT 16
+#endif
+constexpr int kUB = MPC_UB;           // threads of the unit kernels (K_left, K_ins)
+constexpr int kEPT = MPC_EPT;         // events per thread per unit (loads batched)
 constexpr int kUnit = kUB * kEPT;     // events per work unit
 
 struct UnitArgs {

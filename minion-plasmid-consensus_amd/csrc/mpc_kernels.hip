@@ -45,7 +45,10 @@ constexpr int kInsInline = 4;       // insertions up to this length travel as on
 constexpr int kMaxRefLen = (1 << 20) - 2;  // 32-bit coordinates: advances are clamped at kAdvCap > n
 constexpr int kAdvCap = 1 << 20;    // > any reference length: a clamped advance keeps i past the end
 constexpr int kICap = 1 << 28;      // saturation of the running coordinate i
-constexpr int kBW = 16;             // gaps per insertion bucket (K_left workgroup)
+#ifndef MPC_BW
+#define MPC_BW 64
+#endif
+constexpr int kBW = MPC_BW;         // gaps per insertion bucket (K_left workgroup)
 constexpr int kKMax = 8;            // runs per gap tallied in K_left's LDS (others go to HBM)
 constexpr uint32_t kNullGap = 0x3fffffu;
 
@@ -1200,26 +1203,52 @@ struct UnitArgs {
   int32_t nbs;
 };
 
-// one wave per table entry
-__device__ __forceinline__ void units_entry(const UnitArgs& a, int64_t ent) {
-  const int l = lane();
-  if (ent >= a.n_bc) return;
-  const int4 bc = a.bc[ent];
-  int t = 0;
-  for (int pw = bc.z + l; pw < bc.w; pw += 64) t += a.bk_cnt[(int64_t)pw * a.nbs + bc.y];
-  t = wave_sum(t);
-  const int nu = (t + kUnit - 1) / kUnit;
-  if (nu == 0) return;
-  uint32_t u0 = 0;
-  if (l == 0) u0 = atomicAdd(&a.status[MPC_ST_UNITS], (uint32_t)nu);
-  u0 = (uint32_t)__shfl((int)u0, 0, 64);
-  if ((int64_t)u0 + nu > a.units_cap) {
-    if (l == 0) atomicOr(&a.status[MPC_ST_FLAGS], DE_INTERNAL);
-    return;
+// kUE consecutive table entries per wave (one wave per entry at a time), one
+// add to the unit counter per block: a single counter word serializes its
+// atomics (~90 per us), and C5 has 45k entries
+constexpr int kUE = 4;
+constexpr int kUnitEntriesPerBlock = (kRS / 64) * kUE;
+__device__ __forceinline__ void units_block(const UnitArgs& a, int64_t blk) {
+  __shared__ int32_t s_wu[kRS / 64];
+  __shared__ uint32_t s_ubase;
+  const int l = lane(), w = threadIdx.x >> 6;
+  const int64_t ent0 = blk * kUnitEntriesPerBlock + (int64_t)w * kUE;
+  int ts[kUE], nus[kUE], wsum = 0;
+#pragma unroll
+  for (int e = 0; e < kUE; ++e) {
+    const int64_t ent = ent0 + e;
+    int t = 0;
+    if (ent < a.n_bc) {  // wave-uniform
+      const int4 bc = a.bc[ent];
+      for (int pw = bc.z + l; pw < bc.w; pw += 64) t += a.bk_cnt[(int64_t)pw * a.nbs + bc.y];
+      t = wave_sum(t);
+    }
+    ts[e] = t;
+    nus[e] = (t + kUnit - 1) / kUnit;
+    wsum += nus[e];
   }
-  for (int i = l; i < nu; i += 64) {
-    const int e0 = i * kUnit;
-    a.units[u0 + i] = make_int4((int)ent, e0, t - e0 < kUnit ? t - e0 : kUnit, 0);
+  if (l == 0) s_wu[w] = wsum;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int k = 0; k < kRS / 64; ++k) { const int v = s_wu[k]; s_wu[k] = tot; tot += v; }
+    s_ubase = tot ? atomicAdd(&a.status[MPC_ST_UNITS], (uint32_t)tot) : 0u;
+  }
+  __syncthreads();
+  int64_t u0 = (int64_t)s_ubase + s_wu[w];
+#pragma unroll
+  for (int e = 0; e < kUE; ++e) {
+    const int nu = nus[e];
+    if (nu == 0) continue;
+    if (u0 + nu > a.units_cap) {
+      if (l == 0) atomicOr(&a.status[MPC_ST_FLAGS], DE_INTERNAL);
+      return;
+    }
+    for (int i = l; i < nu; i += 64) {
+      const int e0 = i * kUnit;
+      a.units[u0 + i] = make_int4((int)(ent0 + e), e0, ts[e] - e0 < kUnit ? ts[e] - e0 : kUnit, 0);
+    }
+    u0 += nu;
   }
 }
 
@@ -1228,7 +1257,7 @@ __device__ __forceinline__ void units_entry(const UnitArgs& a, int64_t ent) {
 // units (one table entry per wave).  Block-uniform branch.
 __global__ __launch_bounds__(kRS) void K_rsplit_units(Dev d, UnitArgs ua, int32_t nrb) {
   if ((int32_t)blockIdx.x < nrb) rsplit_block(d, blockIdx.x);
-  else units_entry(ua, ((int64_t)blockIdx.x - nrb) * (kRS / 64) + (threadIdx.x >> 6));
+  else units_block(ua, (int64_t)blockIdx.x - nrb);
 }
 
 // Per unit: the entry's <= 256 slices (counts, sources) lane-parallel, block
@@ -1273,7 +1302,7 @@ __device__ __forceinline__ int64_t unit_event_src(const int32_t* s_pre, const in
   return s_src[lo] + (e - s_pre[lo]);
 }
 
-// per gap of a unit's 16-gap bucket: global run range and this shard's sorted-RIGHT range
+// per gap of a unit's bucket (kBW gaps): global run range and this shard's sorted-RIGHT range
 __device__ __forceinline__ void load_bucket_gaps(const int32_t* right_start, const int32_t* rsl, const int32_t* roff,
                                                  int64_t g0, int ngap, int32_t* s_rs, int32_t* s_rsl, int32_t* s_roff) {
   if ((int)threadIdx.x <= ngap) {
@@ -1287,7 +1316,7 @@ __device__ __forceinline__ void load_bucket_gaps(const int32_t* right_start, con
 // K_left: LEFT events -> per-run max length M (the slot layout's input; the
 // bases themselves are tallied on rows once the layout is known).
 //  * insertions: persistent workgroups over the work units; a unit's events
-//    all lie in one 16-gap bucket, so its (gap, run) maxima live in LDS (runs
+//    all lie in one kBW-gap bucket, so its (gap, run) maxima live in LDS (runs
 //    k < kKMax; rarer runs go to HBM) and are flushed with atomics
 //  * long insertions and upstream flanks (one per read, LEFT at gap tstart,
 //    :303): grid-stride, wave-aggregated atomicMax (most reads share gap 0)
@@ -1530,7 +1559,7 @@ __global__ __launch_bounds__(kGB) void K_assemble(Dev d) {
 // ---------------------------------------------------------------------------
 // Slot tallies of the even positions (:37-72 applied to insertion strings).
 // Every inserted base lands in the slot block of its anchor gap, so a work
-// unit (insertion events of one 16-gap bucket) tallies the bucket's row range
+// unit (insertion events of one kBW-gap bucket) tallies the bucket's row range
 // in a dense LDS histogram, then flushes with global atomics (hot buckets are
 // split over several units).  A grid-stride tail adds the long insertions.
 // ---------------------------------------------------------------------------
@@ -1919,7 +1948,11 @@ __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
     __syncthreads();
     if (threadIdx.x == 0) {
       const int32_t m = max(max(s_w[0], s_w[1]), max(s_w[2], s_w[3]));
-      if (m >= 0) atomicMax(d.maxdepth + s_blk[0], (uint32_t)m);
+      // skip the atomic when a value of this run already covers m (the maxima
+      // only grow; a cached read is never above the true one): all blocks'
+      // atomics on the few maxdepth words serialize (C5: 6k blocks)
+      if (m >= 0 && (uint32_t)m > __hip_atomic_load(d.maxdepth + s_blk[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(d.maxdepth + s_blk[0], (uint32_t)m);
     }
   }
 }
@@ -2480,7 +2513,7 @@ int mpc_index(mpc_plan* p, void* stream) {
   const int32_t nrb = (int32_t)((p->N + kRS - 1) / kRS);
   // the insertion work units need only the parse: cut in the RIGHT-split launch
   // (one stream: a second one's event fork/join cost more than the overlap, measured)
-  const int32_t nub = (int32_t)((p->n_bc + kRS / 64 - 1) / (kRS / 64));  // unit-cutting blocks
+  const int32_t nub = (int32_t)((p->n_bc + kUnitEntriesPerBlock - 1) / kUnitEntriesPerBlock);  // unit-cutting blocks
   if (nrb + nub > 0) hipLaunchKernelGGL(K_rsplit_units, dim3(nrb + nub), dim3(kRS), 0, st, d, unit_args(p, d), nrb);
   hipLaunchKernelGGL(K_rsort, dim3(1), dim3(kRS), 0, st, d, nrb, (int32_t)p->end_bit);
   hipLaunchKernelGGL(K_rstart, dim3(nblk(std::max<int64_t>(p->G + 1, p->N))), dim3(256), 0, st, d);  // (M <= N)

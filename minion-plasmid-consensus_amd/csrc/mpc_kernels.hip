@@ -1876,8 +1876,11 @@ __device__ __forceinline__ int sample_of_row_lds(const Dev& d, const int32_t* sr
   return lo;
 }
 
-constexpr int kCR = 1;          // rows per thread of K_call (more blocks: the kernel is latency-bound)
-constexpr int kCB = 256 * kCR;  // rows per K_call block
+// rows per thread of K_call: 1 while the grid is small (the kernel is
+// latency-bound: more blocks), kCRBig for large pileups, where every block's
+// max-depth atomic on the few maxdepth words serializes (C5: 5.7k blocks)
+constexpr int kCRBig = 8;
+constexpr int64_t kCallBlocksMax = 512;  // (the 70 kb parity case takes the kCRBig path)
 
 // per slot: sorted(tuples in dict order, key=count)[::-1] -> top / second / tie -> N (:363-423)
 __device__ __forceinline__ uint4 call_slot(uint4 cv, double gtf, uint32_t* total_out) {
@@ -1907,7 +1910,9 @@ __device__ __forceinline__ uint4 call_slot(uint4 cv, double gtf, uint32_t* total
 }
 
 // calls of every row + max depth over slot 0 (:332-341); rows t + 256 k of the block
+template <int kCR>
 __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
+  constexpr int kCB = 256 * kCR;  // rows per block
   __shared__ int32_t srow[kSmpLds];
   __shared__ int32_t s_blk[2], s_w[4];
   const bool cap = (d.status[MPC_ST_FLAGS] & DE_CAP) != 0;
@@ -1929,21 +1934,25 @@ __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
     mt[k] = row < need ? d.meta[row] : 0;
   }
   __syncthreads();
-  const bool one = s_blk[0] == s_blk[1];
-  int32_t mx = -1;
+  int32_t dep[kCR];  // slot-0 depth of the row (:336), -1: none
 #pragma unroll
   for (int k = 0; k < kCR; ++k) {
     const int64_t row = b0 + threadIdx.x + 256 * k;
     uint32_t total = 0;
     const uint4 out = call_slot(cv[k], d.gtf, &total);
     if (row < R) reinterpret_cast<uint4*>(d.res)[row] = out;
-    if (total > 0 && (mt[k] & 2u)) {  // slot 0 only (:336)
-      if (one) mx = (int32_t)total > mx ? (int32_t)total : mx;
-      else atomicMax(d.maxdepth + sample_of_row_lds(d, srow, row), total);
-    }
+    dep[k] = (total > 0 && (mt[k] & 2u)) ? (int32_t)total : -1;
   }
-  if (one) {  // the block's rows are one sample: one atomic per block
+  // one atomic per (block, sample): atomics on the few maxdepth words serialize
+  for (int sb = s_blk[0]; sb <= s_blk[1]; ++sb) {  // block-uniform
+    int32_t mx = -1;
+#pragma unroll
+    for (int k = 0; k < kCR; ++k) {
+      const int64_t row = b0 + threadIdx.x + 256 * k;
+      if (dep[k] > mx && (s_blk[0] == s_blk[1] || sample_of_row_lds(d, srow, row) == sb)) mx = dep[k];
+    }
     mx = wave_max(mx);
+    __syncthreads();
     if (lane() == 0) s_w[threadIdx.x >> 6] = mx;
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -1951,8 +1960,8 @@ __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
       // skip the atomic when a value of this run already covers m (the maxima
       // only grow; a cached read is never above the true one): all blocks'
       // atomics on the few maxdepth words serialize (C5: 6k blocks)
-      if (m >= 0 && (uint32_t)m > __hip_atomic_load(d.maxdepth + s_blk[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-        atomicMax(d.maxdepth + s_blk[0], (uint32_t)m);
+      if (m >= 0 && (uint32_t)m > __hip_atomic_load(d.maxdepth + sb, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+        atomicMax(d.maxdepth + sb, (uint32_t)m);
     }
   }
 }
@@ -1987,6 +1996,8 @@ __global__ __launch_bounds__(256) void K_keep(Dev d, int64_t R) {
 
 __global__ __launch_bounds__(256) void K_emit(Dev d, int64_t R) {
   __shared__ int32_t s_red[4], s_w[4];
+  __shared__ int32_t srow[kSmpLds];
+  load_sample_rows(d, srow);  // (ordered before use by the barriers below)
   const int64_t nb = (R + kKB - 1) / kKB;
   int64_t pre = 0, all = 0;
   for (int64_t k = threadIdx.x; k < nb; k += blockDim.x) {
@@ -2022,7 +2033,7 @@ __global__ __launch_bounds__(256) void K_emit(Dev d, int64_t R) {
   // ncalls[s] = calls before the first row of sample s; ncalls[S] = all
   const int64_t b0 = (int64_t)blockIdx.x * kKB;
   for (int s = 0; s < d.S; ++s) {
-    const int64_t rb = d.row_base[d.gbase[s]];
+    const int64_t rb = s < kSmpLds ? srow[s] : d.row_base[d.gbase[s]];
     if (rb >= b0 && rb < b0 + kKB && (rb - b0) / 4 == threadIdx.x) {
       int64_t q = pre + wpre + inc - c;
       for (int k = 0; k < (int)((rb - b0) & 3); ++k) q += (bits >> k) & 1u;
@@ -2569,7 +2580,8 @@ int mpc_consensus(mpc_plan* p, double mdf, double gtf, void* stream) {
   d.mdf = mdf;
   d.gtf = gtf;
   const int64_t R = p->row_cap;
-  hipLaunchKernelGGL(K_call, dim3(nblk(R, kCB)), dim3(256), 0, st, d, R);
+  if (nblk(R, 256) > kCallBlocksMax) hipLaunchKernelGGL(K_call<kCRBig>, dim3(nblk(R, 256 * kCRBig)), dim3(256), 0, st, d, R);
+  else hipLaunchKernelGGL(K_call<1>, dim3(nblk(R, 256)), dim3(256), 0, st, d, R);
   hipLaunchKernelGGL(K_keep, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R);
   hipLaunchKernelGGL(K_emit, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R);
   HIPCHK(hipGetLastError());

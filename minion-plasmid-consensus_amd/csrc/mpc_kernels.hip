@@ -199,7 +199,7 @@ __host__ __device__ inline int parse_lds_bytes(int n_max, int tm, int nbmax, int
   const int tallies = tm == 0 ? 0 : tm == 1 ? 12 * (n_max + 1) : tm == 2 ? 8 * (n_max + 1) + 4 * ((n_max + 2) / 2)
                                                                  : 4 * ((n_max + 2) / 2);
   const int buckets = 16 * nbmax + 4;  // epilogue: counts, cursors, chunk counts, chunk offsets
-  return nw * (int)sizeof(WaveLds<WIN>) + parse_misc_bytes() + 4 * parse_hl_words(n_max) +
+  return nw * (int)sizeof(WaveLds<WIN>) + parse_misc_bytes() + 4 * parse_hl_words(n_max) + 4 * nbmax +
          (tallies > buckets ? tallies : buckets);
 }
 
@@ -429,7 +429,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int64_t r0 = wk.y, r1 = wk.z;
   const int n = a.n_of[smp];
   const int gb = a.gbase[smp];
-  uint32_t* uni = hl + parse_hl_words(n);
+  const int nbk = (n + 1 + kBW - 1) / kBW;  // insertion buckets
+  uint32_t* bcnt = hl + parse_hl_words(n);  // [nbk] insertion events per bucket (counted as they are stored)
+  uint32_t* uni = bcnt + nbk;
   constexpr bool fused = TM != 0;           // depth differences in LDS (one address space per instantiation)
   constexpr bool lds_sub = TM == 1 || TM == 2;  // substitution tallies in LDS too
   constexpr bool packed = TM >= 2;
@@ -440,7 +442,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   //          biased by 0x8000: at most 16383 reads per workgroup and 2 per read and
   //          position keep every partial sum inside (0, 0xffff): no carry across halves
   uint32_t* del_l = uni + nsub;
-  for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) hl[k] = 0;
+  for (int k = threadIdx.x; k < parse_hl_words(n) + nbk; k += blockDim.x) hl[k] = 0;  // hl, bcnt
   if (fused)
     for (int k = threadIdx.x; k < nsub + (packed ? (n + 2) / 2 : n + 1); k += blockDim.x)
       uni[k] = (packed && k >= nsub) ? 0x80008000u : 0u;
@@ -747,7 +749,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       }
       const bool ins_inline = kind == 3 && olen_e <= kInsInline && te == 0;
       const uint64_t bins = ballot(ins_inline);
-      if (ins_inline) a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);
+      if (ins_inline) {
+        a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);
+        atomicAdd(bcnt + i / kBW, 1u);
+      }
       if (last) {  // the read's last operation: i_end, downstream check, span
         const int ia = i + adv;
         const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
@@ -834,35 +839,14 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   return;  // timing experiment: no bucket sort (results invalid)
 #endif
   // ---- bucket-sort this workgroup's insertion events by gap (counting sort) ----
-  const int nbk = (n + 1 + kBW - 1) / kBW;
-  uint32_t* bcnt = uni;  // aliases the (flushed) tallies
-  uint32_t* bcur = bcnt + nbk;
-  for (int k = threadIdx.x; k < nbk; k += blockDim.x) bcnt[k] = 0;
-  __syncthreads();
+  // bucket counts: bcnt (main loop); cursors and the scatter's chunk tables alias the flushed tallies
+  uint32_t* bcur = uni;
   const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;
-  // both passes walk the wave regions (wcnt[ww] events at wbase[ww]) in wave
-  // order, coalesced, kEpiB loads in flight per thread
-  constexpr int kEpiB = 4;
+  const int bstride = (int)blockDim.x;
 #ifndef MPC_EPIU
 #define MPC_EPIU 8
 #endif
   constexpr int kEpiU = MPC_EPIU;  // events per thread per staged scatter chunk
-  const int bstride = (int)blockDim.x;
-  for (int ww = 0; ww < nw; ++ww) {
-    const uint64_t* src = a.ins_raw + wbase[ww];
-    const int c = (int)wcnt[ww];
-    for (int k0 = threadIdx.x; k0 < c; k0 += kEpiB * bstride) {
-      uint64_t ev[kEpiB];
-#pragma unroll
-      for (int u = 0; u < kEpiB; ++u) ev[u] = k0 + u * bstride < c ? src[k0 + u * bstride] : ~0ull;
-#pragma unroll
-      for (int u = 0; u < kEpiB; ++u) {
-        const uint32_t gap = (uint32_t)(ev[u] >> 10) & kNullGap;
-        if (gap <= (uint32_t)n) atomicAdd(bcnt + gap / kBW, 1u);
-      }
-    }
-  }
-  __syncthreads();
   if (threadIdx.x < 64) {  // exclusive scan over buckets by one wave
     int carry_b = 0;
     for (int c0 = 0; c0 < nbk; c0 += 64) {

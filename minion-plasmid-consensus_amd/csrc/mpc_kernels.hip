@@ -980,6 +980,7 @@ __device__ __forceinline__ void rsplit_block(const Dev& d, int64_t b) {
 // ---------------------------------------------------------------------------
 constexpr int kRS = 1024;
 constexpr int kSortLds = 8192;
+constexpr int kGatherLds = 2048;  // source blocks whose prefix stays in LDS (entry-parallel gather)
 
 __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t end_bit) {
   __shared__ uint32_t lk[2][kSortLds];
@@ -988,7 +989,9 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
   __shared__ int32_t hb[256];
   __shared__ int32_t s_w[kRS / 64];
   __shared__ int32_t s_carry;
+  __shared__ int32_t s_bpre[kGatherLds + 1];
   const int tid = threadIdx.x, l = lane(), w = tid >> 6;
+  const bool pre_lds = nblocks <= kGatherLds;
   // exclusive prefix of the per-block counts -> bpre[0..nblocks]
   if (tid == 0) s_carry = 0;
   __syncthreads();
@@ -1000,7 +1003,10 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
     __syncthreads();
     int pre = s_carry;
     for (int k = 0; k < w; ++k) pre += s_w[k];
-    if (b < nblocks) d.bpre[b] = pre + inc - v;
+    if (b < nblocks) {
+      d.bpre[b] = pre + inc - v;
+      if (pre_lds) s_bpre[b] = pre + inc - v;
+    }
     __syncthreads();
     if (tid == kRS - 1) s_carry = pre + inc;
     __syncthreads();
@@ -1018,10 +1024,36 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
     kb[(passes + 1) & 1] = d.keys_tmp; vb[(passes + 1) & 1] = d.vals_tmp;
   }
   __syncthreads();
-  // gather (read order) into buffer 0: one source block per thread, 8 loads in
-  // flight per batch (the copies are independent; a serial loop would wait a
-  // full memory latency per entry)
-  for (int b = tid; b < nblocks; b += kRS) {
+  // gather (read order) into buffer 0.  Few source blocks: entry-parallel, the
+  // source block of entry i by a search of the LDS prefix, 8 loads in flight
+  // per thread; else one source block per thread, 8 loads in flight per batch
+  // (the copies are independent; a serial loop would wait a full memory
+  // latency per entry)
+  for (int64_t i0 = 0; pre_lds && i0 < M; i0 += 8 * kRS) {
+    uint32_t kk[8];
+    int32_t vv[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t i = i0 + tid + (int64_t)u * kRS;
+      kk[u] = 0u; vv[u] = 0;
+      if (i < M) {
+        int lo = 0, hi = nblocks - 1;  // last block with s_bpre <= i (it holds >= 1 entry)
+        while (lo < hi) {
+          const int mid = (lo + hi + 1) >> 1;
+          if (s_bpre[mid] <= i) lo = mid; else hi = mid - 1;
+        }
+        const int64_t src = (int64_t)lo * kRS + (i - s_bpre[lo]);
+        kk[u] = d.keys_in[src];
+        vv[u] = d.vals_in[src];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const int64_t i = i0 + tid + (int64_t)u * kRS;
+      if (i < M) { kb[0][i] = kk[u]; vb[0][i] = vv[u]; }
+    }
+  }
+  for (int b = tid; !pre_lds && b < nblocks; b += kRS) {
     const int c = d.bcnt[b];
     const int o = d.bpre[b];
     const uint32_t* ks = d.keys_in + (int64_t)b * kRS;

@@ -1214,7 +1214,8 @@ constexpr int kUnit = kUB * kEPT;     // events per work unit
 
 struct UnitArgs {
   const int4* bc;  // {sample, bucket, pw0, pw1}
-  const int32_t* bk_cnt; int4* units; uint32_t* status;
+  const int32_t* n_of; const int32_t* gbase;
+  const int32_t* bk_cnt; int4* units; uint32_t* status;  // units: 2 int4 per unit (see read_unit)
   int64_t n_bc, units_cap;
   int32_t nbs;
 };
@@ -1230,12 +1231,15 @@ __device__ __forceinline__ void units_block(const UnitArgs& a, int64_t blk) {
   const int l = lane(), w = threadIdx.x >> 6;
   const int64_t ent0 = blk * kUnitEntriesPerBlock + (int64_t)w * kUE;
   int ts[kUE], nus[kUE], wsum = 0;
+  int4 bcs[kUE];
 #pragma unroll
   for (int e = 0; e < kUE; ++e) {
     const int64_t ent = ent0 + e;
     int t = 0;
+    bcs[e] = make_int4(0, 0, 0, 0);
     if (ent < a.n_bc) {  // wave-uniform
       const int4 bc = a.bc[ent];
+      bcs[e] = bc;
       for (int pw = bc.z + l; pw < bc.w; pw += 64) t += a.bk_cnt[(int64_t)pw * a.nbs + bc.y];
       t = wave_sum(t);
     }
@@ -1260,9 +1264,11 @@ __device__ __forceinline__ void units_block(const UnitArgs& a, int64_t blk) {
       if (l == 0) atomicOr(&a.status[MPC_ST_FLAGS], DE_INTERNAL);
       return;
     }
+    const int n = a.n_of[bcs[e].x], gb = a.gbase[bcs[e].x];
     for (int i = l; i < nu; i += 64) {
       const int e0 = i * kUnit;
-      a.units[u0 + i] = make_int4((int)(ent0 + e), e0, ts[e] - e0 < kUnit ? ts[e] - e0 : kUnit, 0);
+      a.units[2 * (u0 + i)] = bcs[e];
+      a.units[2 * (u0 + i) + 1] = make_int4(e0, ts[e] - e0 < kUnit ? ts[e] - e0 : kUnit, n, gb);
     }
     u0 += nu;
   }
@@ -1276,38 +1282,65 @@ __global__ __launch_bounds__(kRS) void K_rsplit_units(Dev d, UnitArgs ua, int32_
   else units_block(ua, (int64_t)blockIdx.x - nrb);
 }
 
-// Per unit: the entry's <= 256 slices (counts, sources) lane-parallel, block
-// scan; afterwards event e of the entry is ins_sorted[s_src[j] + e - s_pre[j]]
-// with j = the last slice whose s_pre <= e.
-struct UnitView { int smp, bucket, e0, cnt; };
-__device__ __forceinline__ UnitView load_unit(const int4* bc_tab, const int4* units, int64_t u,
-                                              const int32_t* bk_cnt, const int32_t* bk_off, const int64_t* rbase,
-                                              int nbs, int32_t* s_pre, int64_t* s_src, int32_t* s_wsum) {
-  const int4 un = units[u];
-  const int4 bc = bc_tab[un.x];
+// A unit record (2 int4, written by units_block): {sample, bucket, pw0, pw1},
+// {e0, cnt, n, gbase}.  Per unit: the entry's <= 256 slices (counts, sources)
+// lane-parallel, block scan; afterwards event e of the entry is
+// ins_sorted[s_src[j] + e - s_pre[j]] with j = the last slice whose s_pre <= e.
+// The per-gap tables of the bucket (global run range, this shard's sorted-RIGHT
+// range; K_ins: the anchor row) are loaded in the same round trip.
+struct UnitView { int smp, bucket, e0, cnt, n, gb, g0, gl; int64_t R0, R1; };
+template <bool ANC>
+__device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, const int32_t* bk_cnt,
+                                              const int32_t* bk_off, const int64_t* rbase, int nbs,
+                                              const int32_t* right_start, const int32_t* rsl, const int32_t* roff,
+                                              const int32_t* row_base, const int32_t* lo_f, const int32_t* rowcnt,
+                                              int32_t* s_pre, int64_t* s_src, int32_t* s_wsum,
+                                              int32_t* s_rs, int32_t* s_rsl, int32_t* s_roff, int32_t* s_anc) {
+  const int4 ua = units[2 * u], ub = units[2 * u + 1];
+  UnitView v;
+  v.smp = ua.x; v.bucket = ua.y; v.e0 = ub.x; v.cnt = ub.y; v.n = ub.z; v.gb = ub.w;
+  v.g0 = v.bucket * kBW;
+  v.gl = v.g0 + kBW - 1 < v.n ? v.g0 + kBW - 1 : v.n;  // last gap of the bucket
   const int l = lane(), w = threadIdx.x >> 6;
-  if (threadIdx.x < 256) {  // <= 256 slices (parse workgroups) per table entry
-    const int pw = bc.z + (int)threadIdx.x;
-    int cnt = 0;
-    int64_t src = 0;
-    if (pw < bc.w) {
-      const int64_t slot = (int64_t)pw * nbs + bc.y;
+  const int tid = (int)threadIdx.x;
+  // all global loads of the unit's tables first (one round trip)
+  int cnt = 0;
+  int64_t src = 0;
+  if (tid < 256) {  // <= 256 slices (parse workgroups) per table entry
+    const int pw = ua.z + tid;
+    if (pw < ua.w) {
+      const int64_t slot = (int64_t)pw * nbs + v.bucket;
       cnt = bk_cnt[slot];
       src = rbase[pw] + bk_off[slot];
     }
+  }
+  const int64_t gg = (int64_t)v.gb + v.g0 + tid;
+  const bool gap_t = tid <= v.gl + 1 - v.g0;  // the bucket's gaps and the one after (range ends)
+  const bool anc_t = tid <= v.gl - v.g0;
+  v.R0 = v.R1 = 0;
+  if (ANC) {  // the bucket's row range (K_ins)
+    v.R0 = row_base[(int64_t)v.gb + v.g0];
+    v.R1 = (int64_t)row_base[(int64_t)v.gb + v.gl] + rowcnt[(int64_t)v.gb + v.gl];
+  }
+  int32_t x_rs = 0, x_rsl = 0, x_roff = 0, x_anc = 0;
+  if (gap_t) { x_rs = right_start[gg]; x_rsl = rsl[gg]; x_roff = roff[gg]; }
+  if (ANC && anc_t) x_anc = row_base[gg] + lo_f[gg] - 1;  // + hi of the run
+  if (gap_t) { s_rs[tid] = x_rs; s_rsl[tid] = x_rsl; s_roff[tid] = x_roff; }
+  if (ANC && anc_t) s_anc[tid] = x_anc;
+  if (tid < 256) {
     const int inc = wave_scan_i32(cnt);
     if (l == 63) s_wsum[w] = inc;
-    s_pre[threadIdx.x] = inc - cnt;
-    s_src[threadIdx.x] = src;
+    s_pre[tid] = inc - cnt;
+    s_src[tid] = src;
   }
   __syncthreads();
-  if (threadIdx.x < 256) {
+  if (tid < 256) {
     int wpre = 0;
     for (int k = 0; k < w; ++k) wpre += s_wsum[k];
-    s_pre[threadIdx.x] += wpre;
+    s_pre[tid] += wpre;
   }
   __syncthreads();
-  return UnitView{bc.x, bc.y, un.y, un.z};
+  return v;
 }
 __device__ __forceinline__ int64_t unit_event_src(const int32_t* s_pre, const int64_t* s_src, int e) {
   int lo = 0, hi = 255;  // last slice j with s_pre[j] <= e
@@ -1318,15 +1351,6 @@ __device__ __forceinline__ int64_t unit_event_src(const int32_t* s_pre, const in
   return s_src[lo] + (e - s_pre[lo]);
 }
 
-// per gap of a unit's bucket (kBW gaps): global run range and this shard's sorted-RIGHT range
-__device__ __forceinline__ void load_bucket_gaps(const int32_t* right_start, const int32_t* rsl, const int32_t* roff,
-                                                 int64_t g0, int ngap, int32_t* s_rs, int32_t* s_rsl, int32_t* s_roff) {
-  if ((int)threadIdx.x <= ngap) {
-    s_rs[threadIdx.x] = right_start[g0 + threadIdx.x];
-    s_rsl[threadIdx.x] = rsl[g0 + threadIdx.x];
-    s_roff[threadIdx.x] = roff[g0 + threadIdx.x];
-  }
-}
 
 // ---------------------------------------------------------------------------
 // K_left: LEFT events -> per-run max length M (the slot layout's input; the
@@ -1361,13 +1385,11 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
     for (int k = threadIdx.x; k < kBW * kKMax; k += blockDim.x) (&Ml[0][0])[k] = 0;
-    const UnitView uv = load_unit(a.bc, a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, s_pre, s_src, s_wsum);
-    const int n = a.n_of[uv.smp];
-    const int gb = a.gbase[uv.smp];
-    const int g0 = uv.bucket * kBW;
-    const int gl = g0 + kBW - 1 < n ? g0 + kBW - 1 : n;
-    load_bucket_gaps(a.right_start, a.rsl, a.roff, (int64_t)gb + g0, gl + 1 - g0, s_rs, s_rsl, s_roff);
-    __syncthreads();
+    const UnitView uv = load_unit<false>(a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, a.right_start, a.rsl,
+                                         a.roff, nullptr, nullptr, nullptr, s_pre, s_src, s_wsum, s_rs, s_rsl, s_roff, nullptr);
+    const int n = uv.n;
+    const int gb = uv.gb;
+    const int g0 = uv.g0;
     uint64_t evs[kEPT];
 #pragma unroll
     for (int q = 0; q < kEPT; ++q) {  // all loads first (latency), then the tallies
@@ -1605,15 +1627,13 @@ __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
   // (K_units raises DE_INTERNAL instead of overrunning the unit list)
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
-    const UnitView uv = load_unit(a.bc, a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, s_pre, s_src, s_wsum);
-    const int n = a.n_of[uv.smp];
-    const int64_t gb = a.gbase[uv.smp];
-    const int g0 = uv.bucket * kBW;
-    const int gl = (g0 + kBW - 1 < n ? g0 + kBW - 1 : n);  // last gap of the bucket
-    load_bucket_gaps(a.right_start, a.rsl, a.roff, gb + g0, gl + 1 - g0, s_rs, s_rsl, s_roff);
-    if (tid <= gl - g0) s_anc[tid] = a.row_base[gb + g0 + tid] + a.lo_f[gb + g0 + tid] - 1;  // + hi of the run
-    const int64_t R0 = a.row_base[gb + g0];
-    const int64_t R1 = (int64_t)a.row_base[gb + gl] + a.rowcnt[gb + gl];
+    const UnitView uv = load_unit<true>(a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, a.right_start, a.rsl, a.roff,
+                                        a.row_base, a.lo_f, a.rowcnt, s_pre, s_src, s_wsum, s_rs, s_rsl, s_roff, s_anc);
+    const int n = uv.n;
+    const int64_t gb = uv.gb;
+    const int g0 = uv.g0;
+    const int gl = uv.gl;
+    const int64_t R0 = uv.R0, R1 = uv.R1;
     const bool dense = R1 - R0 <= kFlankRows;
     if (dense)
       for (int k = tid; k < (int)(R1 - R0) * 4; k += blockDim.x) cnt[k] = 0;
@@ -2192,6 +2212,7 @@ static UnitArgs unit_args(const mpc_plan* p, const Dev& d) {
   UnitArgs a;
   a.bc = at<const int4>(p, mpc_plan::B_WBC); a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT);
   a.units = at<int4>(p, mpc_plan::B_UNITS); a.status = d.status;
+  a.n_of = d.n_of; a.gbase = d.gbase;
   a.n_bc = p->n_bc; a.units_cap = p->units_cap; a.nbs = p->nbmax;
   return a;
 }
@@ -2428,7 +2449,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_MAXD, p->S, 4);
   set(mpc_plan::B_WPARSE, (int64_t)p->work_parse.size(), 4);
   set(mpc_plan::B_WBC, (int64_t)p->work_bc.size(), 4);
-  set(mpc_plan::B_UNITS, p->units_cap * 4, 4);
+  set(mpc_plan::B_UNITS, p->units_cap * 8, 4);  // 2 int4 per unit
   size_t o = 0;
   for (int b = 0; b < mpc_plan::B_COUNT; ++b) {
     o = (o + 255) & ~(size_t)255;

@@ -107,6 +107,7 @@ struct Dev {  // device-side views of the plan for the small kernels (passed by 
   int32_t* lo_f; int32_t* rowcnt; int32_t* row_base;
   int32_t* bsum;                     // [2 * ceil(G / kGB)] block sums of rowcnt, diff
   uint32_t* rows; uint8_t* meta; int64_t row_cap;
+  uint32_t* runt;                    // [Ng+G][4][4] per run: inline insertion bases by slot from the right end
   uint32_t* res; int32_t* keep; int32_t* ksum; uint32_t* calls; int32_t* ncalls; uint32_t* maxdepth;
   double mdf, gtf;
 };
@@ -1369,7 +1370,7 @@ struct LeftArgs {
   int64_t N, read_offset, ovf_cap;
   int32_t nbs;
   const int32_t* right_start; const int32_t* rsl; const int32_t* roff; const int32_t* vals_out;
-  int32_t* M;
+  int32_t* M; uint32_t* runt;
   const Ovf* ovf; const uint32_t* ovf_cnt;
 };
 
@@ -1381,10 +1382,12 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
   __shared__ int64_t s_src[256];
   __shared__ int32_t s_wsum[4];
   __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1];  // per gap of the bucket (K_left)
+  __shared__ uint32_t Tl[kBW][kKMax][16];  // per (gap, run): inline bases [bi from the 3' end][code]
   // (K_units raises DE_INTERNAL instead of overrunning the unit list)
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
     for (int k = threadIdx.x; k < kBW * kKMax; k += blockDim.x) (&Ml[0][0])[k] = 0;
+    for (int k = threadIdx.x; k < kBW * kKMax * 16; k += blockDim.x) (&Tl[0][0][0])[k] = 0;
     const UnitView uv = load_unit<false>(a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, a.right_start, a.rsl,
                                          a.roff, nullptr, nullptr, nullptr, s_pre, s_src, s_wsum, s_rs, s_rsl, s_roff, nullptr);
     const int n = uv.n;
@@ -1407,14 +1410,27 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
       const int p = gap - g0;
       const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
       const int64_t k = s_roff[p] + (lb > la ? lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la : 0);
-      if (k < kKMax) atomicMax(&Ml[p][k], (uint32_t)L);
-      else atomicMax(a.M + s_rs[p] + g + k, L);
+      // the bases too, run-relative (LEFT: base bi from the 3' end lands on the
+      // run's slot hi_run - 1 - bi, :37-62): K_ins maps them to rows after the layout
+      if (k < kKMax) {
+        atomicMax(&Ml[p][k], (uint32_t)L);
+        for (int j = 0; j < L; ++j) atomicAdd(&Tl[p][k][4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u)], 1u);
+      } else {
+        atomicMax(a.M + s_rs[p] + g + k, L);
+        uint32_t* rt = a.runt + (s_rs[p] + g + k) * 16;
+        for (int j = 0; j < L; ++j) atomicAdd(rt + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
+      }
     }
     __syncthreads();
     for (int q = threadIdx.x; q < kBW * kKMax; q += blockDim.x) {
       const int k = q % kKMax, p = q / kKMax;
       const uint32_t m = Ml[p][k];
       if (m) atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + k, (int32_t)m);
+    }
+    for (int q = threadIdx.x; q < kBW * kKMax * 16; q += blockDim.x) {  // contiguous per (gap, run)
+      const uint32_t v = (&Tl[0][0][0])[q];
+      const int k = (q >> 4) % kKMax, p = (q >> 4) / kKMax;
+      if (v) atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + k) * 16 + (q & 15), v);
     }
     __syncthreads();
   }
@@ -1612,67 +1628,41 @@ struct InsArgs {
   const int32_t* right_start; const int32_t* rsl; const int32_t* roff; const int32_t* vals_out;
   const int32_t* row_base; const int32_t* rowcnt; const int32_t* lo_f; const int32_t* hiR;
   uint32_t* rows; const Ovf* ovf; const uint32_t* ovf_cnt; const uint8_t* cs;
+  const uint32_t* runt; int64_t G;
 };
 
 __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
-  __shared__ uint32_t cnt[kFlankRows * 4];
-  __shared__ int32_t s_pre[256];
-  __shared__ int64_t s_src[256];
-  __shared__ int32_t s_wsum[4];
-  __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1], s_anc[kBW];
   const int l = lane();
   const int w = uniform_i32((int)(threadIdx.x >> 6));
-  const int tid = threadIdx.x;
   if (a.status[MPC_ST_FLAGS] & DE_CAP) return;
-  // (K_units raises DE_INTERNAL instead of overrunning the unit list)
-  const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
-  for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
-    const UnitView uv = load_unit<true>(a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, a.right_start, a.rsl, a.roff,
-                                        a.row_base, a.lo_f, a.rowcnt, s_pre, s_src, s_wsum, s_rs, s_rsl, s_roff, s_anc);
-    const int n = uv.n;
-    const int64_t gb = uv.gb;
-    const int g0 = uv.g0;
-    const int gl = uv.gl;
-    const int64_t R0 = uv.R0, R1 = uv.R1;
-    const bool dense = R1 - R0 <= kFlankRows;
-    if (dense)
-      for (int k = tid; k < (int)(R1 - R0) * 4; k += blockDim.x) cnt[k] = 0;
-    __syncthreads();
-    uint64_t evs[kEPT];
+  // inline insertions: K_left left their bases per run, indexed by the slot
+  // from the run's right end; the layout gives the run's rows (one thread per
+  // gap, over the gap's runs; LEFT base bi -> row row_base + lo_f + hi_run - 1 - bi)
+  // wave-interleaved over the blocks (64 consecutive gaps per wave, consecutive
+  // waves on different CUs): a few thousand gaps must not land on a few CUs
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  for (int64_t gw = (int64_t)w * gridDim.x + blockIdx.x; gw * 64 < a.G; gw += nwaves) {
+    const int64_t g = gw * 64 + l;
+    if (g >= a.G) continue;
+    const int64_t t0 = (int64_t)a.right_start[g] + g, t1 = (int64_t)a.right_start[g + 1] + g + 1;
+    const int64_t top = (int64_t)a.row_base[g] + a.lo_f[g] - 1;
+    for (int64_t t = t0; t < t1; ++t) {
+      const uint4* rt = reinterpret_cast<const uint4*>(a.runt + t * 16);
+      uint4 v[4];
 #pragma unroll
-    for (int q = 0; q < kEPT; ++q) {  // all loads first (latency), then the tallies
-      const int e = uv.e0 + tid + q * kUB;
-      evs[q] = e < uv.e0 + uv.cnt ? a.ins_sorted[unit_event_src(s_pre, s_src, e)] : ~0ull;
-    }
+      for (int bi = 0; bi < 4; ++bi) v[bi] = rt[bi];
+      const int64_t rtop = top + a.hiR[t];
 #pragma unroll
-    for (int q = 0; q < kEPT; ++q) {
-      const uint64_t ev = evs[q];
-      const int gap = (int)((ev >> 10) & kNullGap);
-      if (gap > n || gap < g0 || gap > gl) continue;
-      const int p = gap - g0;
-      int64_t anc = s_anc[p];  // LEFT: base bi (from the 3' end) -> row lo + hi_run - 1 - bi
-      if (s_rs[p + 1] > s_rs[p]) {  // mixed gap: run k = RIGHT events of earlier reads (all shards)
-        const int64_t rg = (int64_t)(ev >> 32);
-        const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
-        const int64_t k = s_roff[p] + (lb > la ? lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la : 0);
-        anc += a.hiR[s_rs[p] + gb + gap + k];
-      }
-      const int Li = (int)((ev >> 8) & 3u) + 1;  // inline insertion: 2-bit codes in string order
-      for (int k = 0; k < Li; ++k) {
-        const int code = (int)((ev >> (2 * k)) & 3u);
-        const int64_t row = anc - (Li - 1 - k);
-        if (dense && row >= R0 && row < R1) atomicAdd(cnt + (row - R0) * 4 + code, 1u);
-        else atomicAdd(a.rows + row * 4 + code, 1u);
+      for (int bi = 0; bi < 4; ++bi) {
+        uint32_t* row = a.rows + (rtop - bi) * 4;
+        if (v[bi].x) atomicAdd(row + 0, v[bi].x);
+        if (v[bi].y) atomicAdd(row + 1, v[bi].y);
+        if (v[bi].z) atomicAdd(row + 2, v[bi].z);
+        if (v[bi].w) atomicAdd(row + 3, v[bi].w);
       }
     }
-    __syncthreads();
-    if (dense)
-      for (int k = tid; k < (int)(R1 - R0) * 4; k += blockDim.x) {
-        const uint32_t v = cnt[k];
-        if (v) atomicAdd(a.rows + R0 * 4 + k, v);
-      }
-    __syncthreads();
   }
+  const int64_t nunits = 0;  // (the long-insertion part below starts at block 0)
   // long insertions (grid-stride, LEFT like the short ones; from the first
   // block that had no unit, so they run beside the unit blocks)
   const int64_t nov = *a.ovf_cnt < (uint32_t)a.ovf_cap ? *a.ovf_cnt : a.ovf_cap;
@@ -2114,7 +2104,7 @@ struct mpc_plan {
     B_HASLEFT, B_KIN, B_VIN, B_KOUT, B_VOUT, B_KTMP, B_VTMP, B_BCNT, B_BPRE, B_RLEN, B_RPOS, B_RSTART, B_RSLOC, B_ROFF, B_RCNT, B_RCNTALL,
     // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
     B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
-    B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_COUNT
+    B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_RUNT, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -2144,7 +2134,7 @@ Dev mpc_plan::dev() const {
   d.rsl = at<int32_t>(this, B_RSLOC); d.roff = at<int32_t>(this, B_ROFF); d.rcnt = at<int32_t>(this, B_RCNT);
   d.rcnt_all = at<int32_t>(this, B_RCNTALL); d.shard = shard; d.n_shards = n_shards;
   d.diff = at<int32_t>(this, B_DIFF); d.sub = at<uint32_t>(this, B_SUB);
-  d.M = at<int32_t>(this, B_M); d.runR = at<int32_t>(this, B_RUNR);
+  d.M = at<int32_t>(this, B_M); d.runR = at<int32_t>(this, B_RUNR); d.runt = at<uint32_t>(this, B_RUNT);
   d.hiR = at<int32_t>(this, B_HIR); d.loR = at<int32_t>(this, B_LOR);
   d.lo_f = at<int32_t>(this, B_LOF); d.rowcnt = at<int32_t>(this, B_ROWCNT); d.row_base = at<int32_t>(this, B_ROWBASE);
   d.bsum = at<int32_t>(this, B_BSUM);
@@ -2203,7 +2193,7 @@ static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
   a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
   a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = p->nbmax;
-  a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out; a.M = d.M;
+  a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out; a.M = d.M; a.runt = d.runt;
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt;
   return a;
 }
@@ -2231,6 +2221,7 @@ static InsArgs ins_args(const mpc_plan* p, const Dev& d) {
   a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out;
   a.row_base = d.row_base; a.rowcnt = d.rowcnt; a.lo_f = d.lo_f; a.hiR = d.hiR;
   a.rows = d.rows; a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.cs = d.cs;
+  a.runt = d.runt; a.G = p->G;
   return a;
 }
 
@@ -2450,6 +2441,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_WPARSE, (int64_t)p->work_parse.size(), 4);
   set(mpc_plan::B_WBC, (int64_t)p->work_bc.size(), 4);
   set(mpc_plan::B_UNITS, p->units_cap * 8, 4);  // 2 int4 per unit
+  set(mpc_plan::B_RUNT, RU * 16, 4);            // per run: inline LEFT bases [bi from the 3' end][code]
   size_t o = 0;
   for (int b = 0; b < mpc_plan::B_COUNT; ++b) {
     o = (o + 255) & ~(size_t)255;
@@ -2543,9 +2535,10 @@ int mpc_parse(mpc_plan* p, void* stream) {
     add(d.maxdepth, p->S, 0u);
     add(d.M, p->runs_cap, 0u);
     add(d.runR, p->runs_cap, 0u);
+    add(d.runt, 16 * p->runs_cap, 0u);
     add(d.rows, 4 * p->row_cap, 0u);
     add(d.meta, (int64_t)(p->sz[mpc_plan::B_META] / 4), 0u);
-    const int64_t most = std::max<int64_t>(4 * p->row_cap, std::max<int64_t>(4 * p->G, p->runs_cap));
+    const int64_t most = std::max<int64_t>(4 * p->row_cap, std::max<int64_t>(4 * p->G, 16 * p->runs_cap));
     hipLaunchKernelGGL(K_clear, dim3(std::min<unsigned>(nblk(most, 256), 1024)), dim3(256), 0, st, c);
   }
   if (p->n_parse_wg > 0)

@@ -1612,23 +1612,19 @@ __global__ __launch_bounds__(kGB) void K_assemble(Dev d) {
 
 // ---------------------------------------------------------------------------
 // Slot tallies of the even positions (:37-72 applied to insertion strings).
-// Every inserted base lands in the slot block of its anchor gap, so a work
-// unit (insertion events of one kBW-gap bucket) tallies the bucket's row range
-// in a dense LDS histogram, then flushes with global atomics (hot buckets are
-// split over several units).  A grid-stride tail adds the long insertions.
+// A LEFT string's base bi (from the 3' end) lands on slot hi_run - 1 - bi of
+// its gap, so K_left tallies the inline insertions per (run, bi, base) and
+// K_ins maps every run onto its rows once the layout gives hi_run.  A
+// grid-stride tail adds the long insertions (bases re-read from cs).
 // ---------------------------------------------------------------------------
-constexpr int kFlankRows = 2048;  // dense LDS rows per unit (else HBM atomics)
 
 struct InsArgs {
-  uint32_t* status; const int32_t* sample; const int32_t* n_of; const int32_t* gbase;
-  const int4* bc; const int4* units;
-  const uint64_t* ins_sorted; const int32_t* bk_cnt; const int32_t* bk_off; const int64_t* rbase;
-  int64_t N, read_offset, ovf_cap;
-  int32_t nbs;
+  uint32_t* status; const int32_t* sample; const int32_t* gbase;
+  int64_t read_offset, ovf_cap, G;
   const int32_t* right_start; const int32_t* rsl; const int32_t* roff; const int32_t* vals_out;
-  const int32_t* row_base; const int32_t* rowcnt; const int32_t* lo_f; const int32_t* hiR;
+  const int32_t* row_base; const int32_t* lo_f; const int32_t* hiR;
   uint32_t* rows; const Ovf* ovf; const uint32_t* ovf_cnt; const uint8_t* cs;
-  const uint32_t* runt; int64_t G;
+  const uint32_t* runt;
 };
 
 __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
@@ -1662,12 +1658,9 @@ __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
       }
     }
   }
-  const int64_t nunits = 0;  // (the long-insertion part below starts at block 0)
-  // long insertions (grid-stride, LEFT like the short ones; from the first
-  // block that had no unit, so they run beside the unit blocks)
+  // long insertions (grid-stride over waves, LEFT like the short ones)
   const int64_t nov = *a.ovf_cnt < (uint32_t)a.ovf_cap ? *a.ovf_cnt : a.ovf_cap;
-  const int64_t fb = ((int64_t)blockIdx.x + gridDim.x - nunits % gridDim.x) % gridDim.x;
-  for (int64_t t = fb * (kUB / 64) + w; t < nov; t += (int64_t)gridDim.x * (kUB / 64)) {
+  for (int64_t t = (int64_t)blockIdx.x * (kUB / 64) + w; t < nov; t += (int64_t)gridDim.x * (kUB / 64)) {
     const Ovf o = a.ovf[t];
     const int64_t g = a.gbase[a.sample[o.read]] + o.gap;
     const int64_t run = run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + o.read);
@@ -2212,16 +2205,12 @@ static int64_t flank_grid(const mpc_plan* p) { return std::max<int64_t>(1, (p->N
 
 static InsArgs ins_args(const mpc_plan* p, const Dev& d) {
   InsArgs a;
-  a.status = d.status; a.sample = d.sample; a.n_of = d.n_of; a.gbase = d.gbase;
-  a.bc = at<const int4>(p, mpc_plan::B_WBC); a.units = at<const int4>(p, mpc_plan::B_UNITS);
-  a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
-  a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
-  a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
-  a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = p->nbmax;
+  a.status = d.status; a.sample = d.sample; a.gbase = d.gbase;
+  a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.G = p->G;
   a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out;
-  a.row_base = d.row_base; a.rowcnt = d.rowcnt; a.lo_f = d.lo_f; a.hiR = d.hiR;
+  a.row_base = d.row_base; a.lo_f = d.lo_f; a.hiR = d.hiR;
   a.rows = d.rows; a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.cs = d.cs;
-  a.runt = d.runt; a.G = p->G;
+  a.runt = d.runt;
   return a;
 }
 

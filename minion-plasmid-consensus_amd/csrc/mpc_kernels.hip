@@ -1624,13 +1624,13 @@ struct InsArgs {
   const int32_t* right_start; const int32_t* rsl; const int32_t* roff; const int32_t* vals_out;
   const int32_t* row_base; const int32_t* lo_f; const int32_t* hiR;
   uint32_t* rows; const Ovf* ovf; const uint32_t* ovf_cnt; const uint8_t* cs;
-  const uint32_t* runt;
+  uint32_t* runt;
 };
 
 __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
   const int l = lane();
   const int w = uniform_i32((int)(threadIdx.x >> 6));
-  if (a.status[MPC_ST_FLAGS] & DE_CAP) return;
+  const bool cap = (a.status[MPC_ST_FLAGS] & DE_CAP) != 0;  // rows too small: only clear runt
   // inline insertions: K_left left their bases per run, indexed by the slot
   // from the run's right end; the layout gives the run's rows (one thread per
   // gap, over the gap's runs; LEFT base bi -> row row_base + lo_f + hi_run - 1 - bi)
@@ -1643,10 +1643,13 @@ __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
     const int64_t t0 = (int64_t)a.right_start[g] + g, t1 = (int64_t)a.right_start[g + 1] + g + 1;
     const int64_t top = (int64_t)a.row_base[g] + a.lo_f[g] - 1;
     for (int64_t t = t0; t < t1; ++t) {
-      const uint4* rt = reinterpret_cast<const uint4*>(a.runt + t * 16);
+      uint4* rt = reinterpret_cast<uint4*>(a.runt + t * 16);
       uint4 v[4];
 #pragma unroll
       for (int bi = 0; bi < 4; ++bi) v[bi] = rt[bi];
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi) rt[bi] = make_uint4(0u, 0u, 0u, 0u);  // runt is zero for the next K_left
+      if (cap) continue;
       const int64_t rtop = top + a.hiR[t];
 #pragma unroll
       for (int bi = 0; bi < 4; ++bi) {
@@ -1658,6 +1661,7 @@ __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
       }
     }
   }
+  if (cap) return;
   // long insertions (grid-stride over waves, LEFT like the short ones)
   const int64_t nov = *a.ovf_cnt < (uint32_t)a.ovf_cap ? *a.ovf_cnt : a.ovf_cap;
   for (int64_t t = (int64_t)blockIdx.x * (kUB / 64) + w; t < nov; t += (int64_t)gridDim.x * (kUB / 64)) {
@@ -2103,6 +2107,7 @@ struct mpc_plan {
   size_t sz[B_COUNT];
   int64_t cnt[B_COUNT];
   bool bound = false;
+  bool runt_dirty = true;  // runt may hold tallies: K_clear zeroes it (K_ins zeroes what it maps)
   Dev dev() const;
 };
 
@@ -2474,6 +2479,7 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WBC), p->work_bc.data(), 4 * p->work_bc.size(), hipMemcpyHostToDevice));
   HIPCHK(hipFuncSetAttribute(parse_kernel(p->tally_mode, p->parse_win), hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
   p->bound = true;
+  p->runt_dirty = true;
   return MPC_OK;
 }
 
@@ -2524,10 +2530,11 @@ int mpc_parse(mpc_plan* p, void* stream) {
     add(d.maxdepth, p->S, 0u);
     add(d.M, p->runs_cap, 0u);
     add(d.runR, p->runs_cap, 0u);
-    add(d.runt, 16 * p->runs_cap, 0u);
+    if (p->runt_dirty) add(d.runt, 16 * p->runs_cap, 0u);
     add(d.rows, 4 * p->row_cap, 0u);
     add(d.meta, (int64_t)(p->sz[mpc_plan::B_META] / 4), 0u);
-    const int64_t most = std::max<int64_t>(4 * p->row_cap, std::max<int64_t>(4 * p->G, 16 * p->runs_cap));
+    const int64_t most = std::max<int64_t>(4 * p->row_cap, std::max<int64_t>(4 * p->G, (p->runt_dirty ? 16 : 1) * p->runs_cap));
+    p->runt_dirty = false;
     hipLaunchKernelGGL(K_clear, dim3(std::min<unsigned>(nblk(most, 256), 1024)), dim3(256), 0, st, c);
   }
   if (p->n_parse_wg > 0)
@@ -2568,6 +2575,7 @@ int mpc_tally(mpc_plan* p, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
   hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));  // (units: mpc_index)
+  p->runt_dirty = true;  // until K_ins has mapped (and cleared) the run tallies
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -2587,6 +2595,7 @@ int mpc_rows(mpc_plan* p, void* stream) {
   Dev d = p->dev();
   hipLaunchKernelGGL(K_assemble, dim3(nblk(p->G, kGB)), dim3(kGB), 0, st, d);
   hipLaunchKernelGGL(K_ins, dim3(ins_grid(p)), dim3(kUB), 0, st, ins_args(p, d));
+  p->runt_dirty = false;  // K_ins zeroes every run tally it maps (all runs of all gaps)
   if (p->N > 0) hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(256), 0, st, flank_args(p, d));
   HIPCHK(hipGetLastError());
   return MPC_OK;
@@ -2618,6 +2627,7 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
       break;
     case MPC_K_LEFT:
       hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));
+      p->runt_dirty = true;
       break;
     case MPC_K_INS:
       hipLaunchKernelGGL(K_ins, dim3(ins_grid(p)), dim3(kUB), 0, st, ins_args(p, d));

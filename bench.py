@@ -3,27 +3,43 @@
 
   python bench.py [--gpus N] [--steps K] [--warmup W] [--config c2]
 
-A step = one full pass of the hot path (Steps 4-6 of the reference:
-cs parse -> pileup -> consensus calls) over one batch of synthetic, seeded,
-device-resident input.  At N=1 the workload is BASELINE.json configs[1]
-(C2: pUC19-size 2,686 bp plasmid, 100k reads, sense + antisense in one launch).
-With N>1 (torch.distributed.run, one rank per GPU, RCCL) every rank holds a
-C2-sized contiguous read shard of ONE global pileup (weak scaling) and the
-ranks exchange the downstream-event index and the count rows (see
-minion-plasmid-consensus_amd/dist.py).
+A step = one full pass of the hot path (Steps 4-6 of the reference: cs parse
+-> pileup -> consensus calls) over one batch of synthetic, seeded,
+device-resident input.  At N=1 the workload is BASELINE.json configs[1] (C2:
+pUC19-size 2,686 bp plasmid, 100k reads, sense + antisense in one launch).
+
+Multi-GPU (torch.distributed.run, one rank per GPU, RCCL): every config is ONE
+global pileup over ONE read set (same reference, same seed); rank k holds the
+k-th contiguous slice of the global read order (Synth(reads=(a, b)) generates
+exactly those reads of the full set) and the ranks exchange the small per-gap
+/ per-run arrays of minion-plasmid-consensus_amd/dist.py.
+  c1, c2, c4   weak scaling: the global set has N x (reads per GPU) reads
+  c3           strong scaling: 1M reads in total, N slices (BASELINE configs[2])
+  c5           sample-partitioned replicas: 12 plasmids per GPU, no collective
 
 Output: one JSON line (rank 0) with the contract fields plus
   roofline      the dominant kernel (K_parse) vs the HBM roofline: algorithmic
                 bytes (sum of cs bytes + 24 B per read) / its mean
-                duration measured here with HIP events on the launch stream
+                duration measured here with HIP events on the launch stream;
+                traffic = HBM bytes per launch from rocprofv3 PMC passes
+                (profiles/pmc_traffic_<config>.json, scripts/traffic.py)
   cpu_baseline  the C restatement of the reference (oracle/, "port") timed on
-                this host on the full C2 workload, 1 thread (rank 0, N=1 only)
+                this host on a bounded read sample, 1 thread (rank 0, N=1 only),
+                and under "reference" the reference script itself timed in the
+                build container (profiles/ref_cpu_baseline.json,
+                scripts/time_reference.py)
+  e2e           (N=1, c1/c2/c4) the drop-in CLI on files of the same workload:
+                ingest + H2D + kernels + D2H + writers, wall clock
 """
 import argparse
+import contextlib
 import importlib
+import io
 import json
 import os
+import shutil
 import sys
+import tempfile
 import time
 
 import numpy as np
@@ -35,22 +51,111 @@ METRIC = "aligned bases/sec pileup+consensus (1/2/4/8 GPU) and % HBM roofline"
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md chip table (spec)
 
 CONFIGS = {
-    # name: (n, reads per sample per rank, profile, seed, antisense, description)
-    "c2": (2686, 100_000, "default", 2, True,
-           "C2 (BASELINE configs[1]): pUC19-size 2,686 bp plasmid, 100k reads, sense+antisense pileup"),
-    "c1": (5000, 20_000, "default", 1, False,
-           "C1 (BASELINE configs[0]): 5 kb plasmid, 20k reads, sense only"),
-    "c3": (10_000, 125_000, "default", 3, False,
-           "C3 (BASELINE configs[2]): 10 kb plasmid, 1M reads total over 8 GPUs (125k per GPU), sense"),
-    "c4": (10_000, 100_000, "indel", 4, True,
-           "C4 (BASELINE configs[3]): 10 kb, 100k reads, indel-heavy 1/5/5 %, sense+antisense"),
-    # multi-sample: 96 plasmids partitioned over the ranks (12 per GPU at N=8), both strands,
-    # replicas only (no collective); at N=1 one GPU holds the 12 plasmids of rank 0
-    "c5": (30_000, 10_000, "default", 5000, True,
+    # name: (n, reads per sample, per-GPU (weak) or total (strong), profile, seed, antisense, description)
+    "c2": (2686, 100_000, "weak", "default", 2, True,
+           "C2 (BASELINE configs[1]): pUC19-size 2,686 bp plasmid, 100k reads per GPU, sense+antisense pileup"),
+    "c1": (5000, 20_000, "weak", "default", 1, False,
+           "C1 (BASELINE configs[0]): 5 kb plasmid, 20k reads per GPU, sense only"),
+    "c3": (10_000, 1_000_000, "strong", "default", 3, False,
+           "C3 (BASELINE configs[2]): 10 kb plasmid, 1M reads in total sharded over the GPUs, sense"),
+    "c4": (10_000, 100_000, "weak", "indel", 4, True,
+           "C4 (BASELINE configs[3]): 10 kb, 100k reads per GPU, indel-heavy 1/5/5 %, sense+antisense"),
+    "c5": (30_000, 10_000, "weak", "default", 5000, True,
            "C5 (BASELINE configs[4]): 30 kb BAC-size constructs, 12 plasmids x 10k reads per GPU "
            "(96 over 8 GPUs), sense+antisense, sample-partitioned"),
 }
 C5_PER_GPU = 12
+PORT_SAMPLE_BASES = 2_500_000_000  # bound of the live CPU-port timing (~6 s of C at ~4e8 b/s)
+E2E_CONFIGS = ("c1", "c2", "c4")
+
+
+def shard_samples(pkg, cfg, rank, world):
+    """This rank's samples: its slice of the global read set (c1-c4), or its
+    plasmids (c5).  Returns (samples, global reads per sample)."""
+    n, reads, scaling, profile, seed, antisense, _ = CONFIGS[cfg]
+    strands = range(2 if antisense else 1)
+    if cfg == "c5":
+        samples = []
+        for k in range(C5_PER_GPU):
+            syn = pkg.synth.Synth(n=n, n_reads=reads, profile=profile, seed=seed + C5_PER_GPU * rank + k,
+                                  antisense=antisense)
+            samples += [syn.sample(s) for s in strands]
+        return samples, reads
+    total = reads * world if scaling == "weak" else reads
+    a, b = total * rank // world, total * (rank + 1) // world
+    syn = pkg.synth.Synth(n=n, n_reads=total, profile=profile, seed=seed, antisense=antisense, reads=(a, b))
+    return [syn.sample(s) for s in strands], total
+
+
+def port_baseline(samples, mdf, gtf, cfg):
+    """The oracle's C restatement over the first reads of every sample, at most
+    PORT_SAMPLE_BASES aligned bases in total (1 thread)."""
+    sys.path.insert(0, os.path.join(REPO, "oracle"))
+    import oracle  # CPU checker: timed here as the baseline, never on the product path
+    budget = PORT_SAMPLE_BASES // len(samples)
+    cb, nr, tot_reads, t = 0, 0, 0, 0.0
+    for s in samples:
+        al = np.asarray(s["aligned"], dtype=np.int64)
+        k = int(np.searchsorted(np.cumsum(al), budget, side="right")) if al.sum() > budget else len(al)
+        k = max(1, min(k, len(al)))
+        c0 = time.perf_counter()
+        oracle.run_packed(s["ref"], s["cs"], s["cs_off"][: k + 1], s["tstart"][:k], s["up"], s["up_off"][: k + 1],
+                          s["down"], s["down_off"][: k + 1], mdf, gtf)
+        t += time.perf_counter() - c0
+        cb += int(al[:k].sum())
+        nr += k
+        tot_reads += len(al)
+    frac = nr / max(1, tot_reads)
+    return {"value": cb / t, "unit": "aligned bases/s", "cores": 1, "kind": "port",
+            "sample": f"{cfg}: first {nr} of {tot_reads} reads ({100 * frac:.3g} %) over {len(samples)} sample(s), "
+                      f"{cb} aligned bases through oracle/mpc_oracle.c, 1 thread, {t:.2f} s"}
+
+
+def reference_record(cfg):
+    try:
+        rec = json.load(open(os.path.join(REPO, "profiles", "ref_cpu_baseline.json")))
+    except (OSError, ValueError):
+        return None
+    r = rec.get("configs", {}).get(cfg)
+    if r is not None:
+        r = dict(r, host=rec.get("host"))
+    return r
+
+
+def e2e_cli(pkg, cfg, samples_n, reads, seed, profile, antisense, reps=2):
+    """Wall time of the drop-in CLI (both strands in one launch) on files of this
+    config: ingest + H2D + kernels + D2H + writers.  Returns a dict."""
+    cli = importlib.import_module("minion-plasmid-consensus_amd.mapped_paf_read_parser")
+    n = samples_n
+    tmp = tempfile.mkdtemp(prefix="mpc_e2e_")
+    try:
+        syn = pkg.synth.Synth(n=n, n_reads=reads, profile=profile, seed=seed, antisense=antisense)
+        aligned = int(sum(int(syn.sample(s)["aligned"].sum()) for s in range(2 if antisense else 1)))
+        p = lambda f: os.path.join(tmp, f)
+        syn.write_files(p("ref.fa"), p("reads.fa"), p("s0.paf"), p("ref1.fa") if antisense else None,
+                        p("s1.paf") if antisense else None)
+        in_bytes = sum(os.path.getsize(p(f)) for f in os.listdir(tmp))
+        argv = ["--ref", p("ref.fa"), "--reads", p("reads.fa"), "--paf", p("s0.paf"), "--consensus", p("c0.fa"),
+                "--chromat", p("ch0.tsv"), "--accuracies", p("acc0.tsv"), "--min_depth_factor", "0.1",
+                "--global_threshold_factor", "5"]
+        if antisense:
+            argv += ["--also", p("ref1.fa"), p("s1.paf"), p("c1.fa"), p("ch1.tsv"), p("acc1.tsv")]
+        walls = []
+        for _ in range(reps):
+            sink = io.StringIO()
+            t0 = time.perf_counter()
+            with contextlib.redirect_stdout(sink):
+                rc = cli.main(argv)
+            walls.append(time.perf_counter() - t0)
+            if rc != 0:
+                raise RuntimeError(f"CLI exit {rc}")
+        return {"value": aligned / min(walls), "unit": "aligned bases/s", "wall_s": min(walls),
+                "wall_s_first": walls[0], "aligned_bases": aligned, "input_bytes": in_bytes,
+                "what": f"{cfg} files ({'2 strands, --also: one launch' if antisense else '1 strand'}); "
+                        "CLI main(): native ingest of ref/PAF/reads FASTA + H2D + plan + kernels + D2H + "
+                        "writers of the three output files; best of %d (first includes allocations)" % reps}
+    finally:
+        shutil.rmtree(tmp, ignore_errors=True)
 
 
 def main():
@@ -61,8 +166,7 @@ def main():
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-file", default=os.path.join(REPO, "profiles", "pmc_traffic.json"),
-                    help="per-launch HBM bytes of K_parse measured with rocprofv3 --pmc (see profiles/)")
+    ap.add_argument("--no-e2e", action="store_true")
     args = ap.parse_args()
 
     import torch
@@ -85,23 +189,16 @@ def main():
     pkg = importlib.import_module("minion-plasmid-consensus_amd")
     eng = pkg.engine
 
-    n, reads, profile, seed, antisense, desc = CONFIGS[args.config]
-    if args.config == "c5":  # this rank's plasmids (distinct references), both strands
-        samples = []
-        for k in range(C5_PER_GPU):
-            syn = pkg.synth.Synth(n=n, n_reads=reads, profile=profile, seed=seed + C5_PER_GPU * rank + k,
-                                  antisense=antisense)
-            samples += [syn.sample(s) for s in range(2 if antisense else 1)]
-    else:  # every rank generates its own contiguous shard of the global read list
-        syn = pkg.synth.Synth(n=n, n_reads=reads, profile=profile, seed=seed + 7919 * rank, antisense=antisense)
-        samples = [syn.sample(s) for s in range(2 if antisense else 1)]
-    if world > 1 and args.config != "c5":
+    cfg = args.config
+    n, reads, scaling, profile, seed, antisense, desc = CONFIGS[cfg]
+    samples, global_reads = shard_samples(pkg, cfg, rank, world)
+    if world > 1 and cfg != "c5":
         dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
         runner = dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange())
     else:
         runner = eng.Runner(samples, device=local)
     batch = runner.batch
-    aligned = batch.aligned_bases  # weak scaling: every rank holds a C2-sized shard of one pileup
+    aligned = batch.aligned_bases
     coll_dev = "cuda" if backend == "nccl" else "cpu"
     if world > 1:
         t = torch.tensor([aligned], dtype=torch.int64, device=coll_dev)
@@ -145,46 +242,47 @@ def main():
     k_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     runner.step(mdf, gtf)  # leave the plan in a clean state
     torch.cuda.synchronize()
+    runner.check()
+    geo = plan.info()
     alg_bytes = batch.cs_bytes + 24 * batch.n_reads
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
     traffic = None
     try:
-        tr = json.load(open(args.traffic_file))
-        if tr.get("config") == args.config and tr.get("kernel") == "K_parse":
+        tr = json.load(open(os.path.join(REPO, "profiles", f"pmc_traffic_{cfg}.json")))
+        if tr.get("config") == cfg and tr.get("kernel") == "K_parse" and tr.get("n_gpus", 1) == world:
             traffic = tr.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
 
-    cpu = None
+    cpu = e2e = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        sys.path.insert(0, os.path.join(REPO, "oracle"))
-        import oracle  # CPU checker: timed here as the baseline, never on the product path
-        c0 = time.perf_counter()
-        cb = 0
-        for s in samples:
-            oracle.run_packed(s["ref"], s["cs"], s["cs_off"], s["tstart"], s["up"], s["up_off"], s["down"],
-                              s["down_off"], mdf, gtf)
-            cb += int(s["aligned"].sum())
-        cdt = time.perf_counter() - c0
-        cpu = {"value": cb / cdt, "unit": "aligned bases/s", "cores": 1, "kind": "port",
-               "sample": f"full {args.config} workload ({len(samples)} samples x {reads} reads, {cb} aligned bases) "
-                         f"through oracle/mpc_oracle.c, 1 thread, {cdt:.2f} s"}
+        cpu = port_baseline(samples, mdf, gtf, cfg)
+        cpu["reference"] = reference_record(cfg)
+    if rank == 0 and world == 1 and not args.no_e2e and cfg in E2E_CONFIGS:
+        del runner, plan, batch
+        torch.cuda.empty_cache()
+        e2e = e2e_cli(pkg, cfg, n, reads, seed, profile, antisense)
 
     if rank == 0:
         line = {
             "metric": METRIC, "value": value, "unit": "aligned bases/s", "n_gpus": world, "steps": args.steps,
-            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True, "scaling": "weak",
+            "warmup": args.warmup, "ms_per_step": ms, "higher_is_better": True,
+            "scaling": "strong" if scaling == "strong" else "weak",
             "vs_baseline": None, "dtype": "u8",
             "data": "synthetic: seeded cs-tag generator (SURVEY §8(d) profile), device-resident",
-            "config": {"workload": desc, "ref_len": n, "reads_per_sample_per_gpu": reads,
-                       "samples": len(samples), "profile": profile, "aligned_bases_per_step": aligned,
-                       "cs_bytes_per_gpu": batch.cs_bytes, "min_depth_factor": mdf,
-                       "global_threshold_factor": gtf},
+            "config": {"workload": desc, "ref_len": n, "global_reads_per_sample": global_reads,
+                       "local_reads": int(len(samples[0]["tstart"])), "samples_per_gpu": len(samples),
+                       "profile": profile, "aligned_bases_per_step": aligned,
+                       "cs_bytes_gpu0": int(sum(int(s["cs_off"][-1] - s["cs_off"][0]) for s in samples)),
+                       "min_depth_factor": mdf, "global_threshold_factor": gtf,
+                       "parallelism": ("replicas" if cfg == "c5" else "read-shard") + f"x{world}"},
             "roofline": {"bound": "hbm", "kernel": "K_parse", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "mean_launch_us": k_ms * 1e3},
             "cpu_baseline": cpu,
+            "e2e": e2e,
         }
+        line["config"]["parse_geometry"] = geo
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

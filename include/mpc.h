@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MPC_ABI_VERSION 4
+#define MPC_ABI_VERSION 5
 
 /* return codes */
 #define MPC_OK 0
@@ -85,7 +85,7 @@ typedef struct {
   const int32_t* sample;   /* [n_reads] sample id */
   /* ---- host-side sizes ---- */
   int32_t n_samples;
-  const int64_t* h_ref_len;    /* host [n_samples] reference lengths n_s (< 2^22) */
+  const int64_t* h_ref_len;    /* host [n_samples] reference lengths n_s (0 <= n_s <= 2^20 - 2) */
   const int64_t* h_read_begin; /* host [n_samples+1] local reads of sample s: [h_read_begin[s], h_read_begin[s+1]) */
   int64_t n_reads;             /* local reads */
   int64_t cs_bytes;            /* cs_off[n_reads] - cs_off[0] */
@@ -132,6 +132,23 @@ int mpc_plan_destroy(mpc_plan* plan);
 int mpc_plan_workspace_bytes(const mpc_plan* plan, size_t* bytes);
 int mpc_plan_bind(mpc_plan* plan, void* workspace, size_t bytes);
 int mpc_plan_buffer(const mpc_plan* plan, int which, size_t* byte_offset, int64_t* count);
+/* Geometry the planner chose (host-only; tests and bench records).  K_parse
+ * keeps per-position tallies in LDS as 16-bit counters: tally_mode 1 = 12 B per
+ * position, 2 = 10 B (biased depth half), 3 = depth in LDS + global
+ * substitution atomics, 0 = global atomics only.  A parse workgroup never
+ * holds more than reads_per_workgroup_cap reads (16-bit exactness bound). */
+typedef struct {
+  int32_t tally_mode;
+  int32_t parse_window;            /* cs bytes per wave window */
+  int32_t parse_waves;             /* waves per parse workgroup */
+  int32_t parse_lds_bytes;
+  int32_t parse_workgroups;
+  int32_t pad_;
+  int64_t max_reads_per_workgroup;
+  int64_t reads_per_workgroup_cap;
+  int64_t workspace_bytes;
+} mpc_plan_info;
+int mpc_plan_get_info(const mpc_plan* plan, mpc_plan_info* info);
 /* update the per-read device pointers (same shape) without re-planning */
 int mpc_plan_set_input(mpc_plan* plan, const mpc_input* in);
 
@@ -163,7 +180,7 @@ int mpc_run(mpc_plan* plan, double min_depth_factor, double global_threshold_fac
 #define MPC_K_PARSE 0
 #define MPC_K_LEFT 2
 #define MPC_K_FLANK 3
-#define MPC_K_INS 4
+#define MPC_K_INS 4  /* consumes (and zeroes) the run tallies K_left left: time it after a K_LEFT */
 int mpc_profile_kernel(mpc_plan* plan, int which, void* stream);
 
 #ifdef __cplusplus

@@ -204,6 +204,12 @@ __host__ __device__ inline int parse_lds_bytes(int n_max, int tm, int nbmax, int
          (tallies > buckets ? tallies : buckets);
 }
 
+// reads per parse workgroup that keep the 16-bit LDS tallies exact: a read adds
+// at most 2 to a position's depth counters; modes 2 / 3 keep the depth
+// difference as one half biased by 0x8000 (|sum| <= 2 * 16383 < 0x8000),
+// mode 1 keeps decrements and increments apart (2 * 32767 < 2^16)
+__host__ __device__ constexpr int64_t wg_reads_cap(int tm) { return tm >= 2 ? 16383 : 32767; }
+
 struct TokInfo { int adv; int kind; uint32_t pay; uint32_t err; };
 
 // Semantics of one token that do not depend on its coordinate, operand read
@@ -399,16 +405,6 @@ __device__ __forceinline__ void chunk_store(uint8_t* p, U8x32 v) {
 // position), insertion events (stored straight into the wave's region of
 // ins_raw), LEFT-gap bits (LDS bitmap).  Epilogue: flush tallies, bucket-sort
 // the insertion events by gap.
-#ifdef MPC_PROF_PARSE
-// instrumentation build only: per-section shader cycles of K_parse summed over waves
-__device__ unsigned long long g_prof[16];
-#define PROF_T(x) const unsigned long long x = __builtin_amdgcn_s_memtime()
-#define PROF_ADD(k, v) pr[k] += (v)
-#else
-#define PROF_T(x)
-#define PROF_ADD(k, v)
-#endif
-
 template <int TM, int WIN>
 __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   constexpr int CH = WIN / 64;
@@ -417,10 +413,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int l = lane();
   const int nw = (int)(blockDim.x >> 6);
   const int w = uniform_i32((int)(threadIdx.x >> 6));
-#ifdef MPC_PROF_PARSE
-  unsigned long long pr[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-  PROF_T(tk0);
-#endif
   WL& W = *reinterpret_cast<WL*>(lds + w * (int)sizeof(WL));
   uint32_t* wcnt = reinterpret_cast<uint32_t*>(lds + nw * (int)sizeof(WL));     // [kMaxPW] events per wave
   int64_t* wbase = reinterpret_cast<int64_t*>(wcnt + kMaxPW);                  // [kMaxPW] event region per wave
@@ -473,7 +465,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   bool carry = false;       // slot 0 holds a read continuing into this window
   WinIn<CH> cur = fetch_window<CH>(a, P, rs0, l);
   while (P < wend) {
-    PROF_T(tw0);
     const int64_t A = P & ~(int64_t)15;
     // ---- window: at most 63 read starts in [P, E) ----
     int64_t E = A + WIN < wend ? A + WIN : wend;
@@ -576,7 +567,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       W.s_read[q] = (int32_t)(rs0 + l);
       W.s_iend[q] = (ts < 0 ? 0 : (ts > n ? n + 1 : ts)) | (dn ? 1 << 30 : 0);
     }
-    PROF_T(tw1);
     // ---- prefetch the next window ----
     const int64_t Pn = C, rsn = rs0 + nst;
     WinIn<CH> nxt;
@@ -630,14 +620,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if (l == 0) W.tok[T] = far ? (uint16_t)(kFar | (c_rs ? 0x8000u : 0u)) : (uint16_t)((C - A) | (c_rs ? 0x8000u : 0u));
     }
     wave_sync_lds();
-    PROF_T(tw2);
 
     // ---- rounds: one token per lane ----
     int32_t G = 0;  // advances of the window's earlier rounds
     int qc = 0;     // read starts of the window's earlier rounds
-#ifdef MPC_EXP_NOROUNDS
-    T = 0;  // timing experiment: window overhead only (results invalid)
-#endif
     for (int t0 = 0; t0 < T; t0 += 64) {
       const int t = t0 + l;
       const bool v = t < T;
@@ -770,8 +756,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       nev += (uint32_t)__popcll(bins);
     }
     wave_sync_lds();
-    PROF_T(tw3);
-    PROF_ADD(0, tw1 - tw0); PROF_ADD(1, tw2 - tw1); PROF_ADD(2, tw3 - tw2); PROF_ADD(4, 1); PROF_ADD(5, (T + 63) / 64);
     // ---- reads that ended in this window: i_end; carry the open one ----
     if (l <= nst && (l > 0 || carry) && W.s_end[l] <= C) a.i_end[W.s_read[l]] = W.s_iend[l] & ~(1 << 30);
     const bool cont = (nst > 0 || carry) && W.s_end[nst] > C;
@@ -788,9 +772,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     P = Pn;
     rs0 = rsn;
     if (Pn < wend) cur = nxt;
-#ifdef MPC_PROF_PARSE
-    { PROF_T(tw4); PROF_ADD(3, tw4 - tw3); }
-#endif
   }
   // reads starting at the range end have an empty cs
   for (int64_t r = rs0 + l; r < rb; r += 64) {
@@ -799,17 +780,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     a.i_end[r] = ts < 0 ? 0 : (ts > n ? n + 1 : ts);
   }
   if (l == 0) { wcnt[w] = nev; wbase[w] = ev_base; }
-#ifdef MPC_PROF_PARSE
-  {
-    PROF_T(tk1);
-    PROF_ADD(6, tk1 - tk0);
-    if (l == 0) for (int k = 0; k < 8; ++k) atomicAdd(&g_prof[k], pr[k]);
-  }
-#endif
   __syncthreads();
-#ifdef MPC_EXP_NOEPI
-  return;  // timing experiment: no flush, no bucket sort (results invalid)
-#endif
   // ---- flush LDS tallies and the LEFT-gap bitmap ----
   if (fused) {
     // one word per lane, consecutive lanes on consecutive words: a wave's
@@ -836,9 +807,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     if (g0 & 31) atomicOr(a.hasleft + (g0 >> 5) + 1, v >> (32 - (g0 & 31)));
   }
   __syncthreads();
-#ifdef MPC_EXP_NOSORT
-  return;  // timing experiment: no bucket sort (results invalid)
-#endif
   // ---- bucket-sort this workgroup's insertion events by gap (counting sort) ----
   // bucket counts: bcnt (main loop); cursors and the scatter's chunk tables alias the flushed tallies
   uint32_t* bcur = uni;
@@ -1811,10 +1779,8 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
       // stage [B0 + c0, B0 + c0 + cn) at stage[(B0 + c0) & 15 ...]
       const int64_t A0 = (B0 + c0) & ~(int64_t)15;
       const int sh0 = (int)((B0 + c0) - A0);
-#ifndef MPC_EXP_NOSTAGE_FLANK
       for (int64_t x = 16 * tid; x < sh0 + cn; x += 16 * blockDim.x)
         *reinterpret_cast<uint4*>(&stage[x]) = *reinterpret_cast<const uint4*>(src + A0 + x);
-#endif
       for (int k = tid; k < kStageB / 32; k += blockDim.x) bm[k] = 0;
       if (tid == 0) {  // owner of the chunk's first byte: last non-empty flank starting <= c0
         int lo = 0, hi = s_nne - 1;
@@ -2093,7 +2059,7 @@ struct mpc_plan {
   uint8_t* ws = nullptr;
   std::vector<int32_t> work_parse, work_bc;  // int4 records
   int n_parse_wg = 0, parse_lds = 0, nbmax = 1, parse_win = 1024, parse_nw = 8;
-  int64_t n_bc = 0, units_cap = 0;
+  int64_t n_bc = 0, units_cap = 0, max_wg_reads = 0;
   int32_t shard = 0, n_shards = 1;
   int tally_mode = 0;  // K_parse TM
   enum {
@@ -2257,17 +2223,6 @@ static inline unsigned nblk(int64_t n, int b = 256) {
 extern "C" {
 
 int mpc_version(void) { return MPC_ABI_VERSION; }
-#ifdef MPC_PROF_PARSE
-int mpc_prof_parse(unsigned long long* out, int reset) {
-  HIPCHK(hipDeviceSynchronize());
-  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_prof), sizeof(unsigned long long) * 16));
-  if (reset) {
-    unsigned long long z[16] = {0};
-    HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_prof), z, sizeof(z)));
-  }
-  return MPC_OK;
-}
-#endif
 const char* mpc_last_error(void) { return g_err.c_str(); }
 
 int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
@@ -2291,7 +2246,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   p->h_gbase.resize(p->S + 1);
   int64_t g = 0;
   for (int s = 0; s < p->S; ++s) {
-    if (p->ref_len[s] < 0 || p->ref_len[s] > kMaxRefLen) { delete p; return fail(MPC_E_ARG, "reference length out of range (< 2^22)"); }
+    if (p->ref_len[s] < 0 || p->ref_len[s] > kMaxRefLen) { delete p; return fail(MPC_E_ARG, "reference length out of range (at most 2^20 - 2 bases)"); }
     p->h_n[s] = (int32_t)p->ref_len[s];
     p->h_gbase[s] = (int32_t)g;
     g += p->ref_len[s] + 1;
@@ -2344,17 +2299,6 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       }
     if (best < 0) { delete p; return fail(MPC_E_ARG, "reference too long for the LDS budget"); }
     p->parse_lds = lds_of(p->parse_win, p->tally_mode, p->parse_nw);
-    if (getenv("MPC_DEBUG_GEOM"))
-      fprintf(stderr, "K_parse geometry: tally mode %d, window %d, %d waves, %d B LDS\n", p->tally_mode, p->parse_win,
-              p->parse_nw, p->parse_lds);
-    if (const char* e = getenv("MPC_PARSE_GEOM")) {  // experiments: "win,nw"
-      int wv = 0, nv = 0;
-      if (sscanf(e, "%d,%d", &wv, &nv) == 2 && (wv == 512 || wv == 1024 || wv == 2048) && nv >= 1 && nv <= kMaxPW &&
-          (p->tally_mode < 2 || wv != 512) && lds_of(wv, p->tally_mode, nv) <= lds_cap) {
-        p->parse_win = wv; p->parse_nw = nv; p->parse_lds = lds_of(wv, p->tally_mode, nv);
-        per_cu = std::max(1, std::min(lds_cap / p->parse_lds, 32 / nv));
-      }
-    }
     const int64_t target = 256 * per_cu;
     std::vector<int> pw_begin(p->S + 1, 0);
     for (int s = 0; s < p->S; ++s) {
@@ -2363,11 +2307,11 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       if (ns <= 0) continue;
       int64_t ch = std::max<int64_t>(1, (target * ns + std::max<int64_t>(p->N, 1) - 1) / std::max<int64_t>(p->N, 1));
       ch = std::min<int64_t>(ch, (ns + 63) / 64);
-      const int64_t wg_reads = p->tally_mode >= 2 ? 16383 : 32767;  // 16-bit LDS tallies (<= 2 per read and position)
-      ch = std::max<int64_t>(ch, (ns + wg_reads - 1) / wg_reads);
+      ch = std::max<int64_t>(ch, (ns + wg_reads_cap(p->tally_mode) - 1) / wg_reads_cap(p->tally_mode));
       for (int64_t c = 0; c < ch; ++c) {
         const int64_t x = a + ns * c / ch, y = a + ns * (c + 1) / ch;
         if (y > x) p->work_parse.insert(p->work_parse.end(), {s, (int32_t)x, (int32_t)y, 0});
+        p->max_wg_reads = std::max<int64_t>(p->max_wg_reads, y - x);
       }
     }
     pw_begin[p->S] = (int)(p->work_parse.size() / 4);
@@ -2448,6 +2392,20 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
 }
 
 int mpc_plan_destroy(mpc_plan* p) { delete p; return MPC_OK; }
+
+int mpc_plan_get_info(const mpc_plan* p, mpc_plan_info* info) {
+  if (!p || !info) return fail(MPC_E_ARG, "null argument");
+  info->tally_mode = p->tally_mode;
+  info->parse_window = p->parse_win;
+  info->parse_waves = p->parse_nw;
+  info->parse_lds_bytes = p->parse_lds;
+  info->parse_workgroups = p->n_parse_wg;
+  info->max_reads_per_workgroup = p->max_wg_reads;
+  info->reads_per_workgroup_cap = wg_reads_cap(p->tally_mode);
+  info->workspace_bytes = (int64_t)p->ws_bytes;
+  info->pad_ = 0;
+  return MPC_OK;
+}
 
 int mpc_plan_workspace_bytes(const mpc_plan* p, size_t* bytes) {
   if (!p || !bytes) return fail(MPC_E_ARG, "null argument");
@@ -2534,8 +2492,9 @@ int mpc_parse(mpc_plan* p, void* stream) {
     add(d.rows, 4 * p->row_cap, 0u);
     add(d.meta, (int64_t)(p->sz[mpc_plan::B_META] / 4), 0u);
     const int64_t most = std::max<int64_t>(4 * p->row_cap, std::max<int64_t>(4 * p->G, (p->runt_dirty ? 16 : 1) * p->runs_cap));
-    p->runt_dirty = false;
     hipLaunchKernelGGL(K_clear, dim3(std::min<unsigned>(nblk(most, 256), 1024)), dim3(256), 0, st, c);
+    HIPCHK(hipGetLastError());
+    p->runt_dirty = false;  // only once the clear is enqueued
   }
   if (p->n_parse_wg > 0)
     launch_parse(p, d, st);
@@ -2595,7 +2554,8 @@ int mpc_rows(mpc_plan* p, void* stream) {
   Dev d = p->dev();
   hipLaunchKernelGGL(K_assemble, dim3(nblk(p->G, kGB)), dim3(kGB), 0, st, d);
   hipLaunchKernelGGL(K_ins, dim3(ins_grid(p)), dim3(kUB), 0, st, ins_args(p, d));
-  p->runt_dirty = false;  // K_ins zeroes every run tally it maps (all runs of all gaps)
+  HIPCHK(hipGetLastError());
+  p->runt_dirty = false;  // K_ins (enqueued) zeroes every run tally it maps (all runs of all gaps)
   if (p->N > 0) hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(256), 0, st, flank_args(p, d));
   HIPCHK(hipGetLastError());
   return MPC_OK;

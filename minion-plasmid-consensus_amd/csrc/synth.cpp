@@ -91,6 +91,10 @@ typedef struct {
   uint64_t seed;
   int32_t antisense;    // also produce sample 1 (alignments to revcomp(ref))
   int32_t n_threads;
+  // generate only reads [read_begin, read_end) of the n_reads-read set (both 0:
+  // all of them).  Every read is keyed by (seed, global index), so the shards of
+  // a multi-GPU run are exact slices of the one global read set.
+  int64_t read_begin, read_end;
 } mpc_synth_params;
 
 struct SynthSample {
@@ -224,8 +228,15 @@ void* mpc_synth_new(const mpc_synth_params* pp) {
   const int ns = p.antisense ? 2 : 1;
   h->s[0].ref = ref;
   if (ns == 2) h->s[1].ref = revcomp(ref);
-  const int64_t N = p.n_reads;
+  int64_t R0 = p.read_begin, R1 = p.read_end;
+  if (R0 == 0 && R1 == 0) R1 = p.n_reads;
+  R0 = std::max<int64_t>(0, std::min<int64_t>(R0, p.n_reads));
+  R1 = std::max<int64_t>(R0, std::min<int64_t>(R1, p.n_reads));
+  h->p.read_begin = R0;
+  h->p.read_end = R1;
+  const int64_t N = R1 - R0;
   int nt = p.n_threads > 0 ? p.n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  nt = std::min(nt, 16);  // the GPU box's CPU share
   nt = (int)std::min<int64_t>(nt, std::max<int64_t>(1, N / 256));
   struct Part {
     std::vector<char> cs[2], up[2], down[2];
@@ -242,7 +253,7 @@ void* mpc_synth_new(const mpc_synth_params* pp) {
     for (int64_t r = r0; r < r1; ++r) {
       int64_t ts, te, nm, al;
       bool minus;
-      gen_read(p, ref, (uint64_t)r, ops, ts, te, up, down, minus, nm, al);
+      gen_read(p, ref, (uint64_t)(R0 + r), ops, ts, te, up, down, minus, nm, al);
       int64_t blen = 0;
       for (auto& o : ops) blen += o.len;
       P.al.push_back(al); P.nm.push_back(nm); P.bl.push_back(blen);
@@ -364,7 +375,7 @@ int mpc_synth_write_files(void* hv, const char* ref_fa, const char* reads_fa, co
                           const char* ref_as_fa, const char* paf1) {
   auto* h = (SynthHandle*)hv;
   const auto& p = h->p;
-  const int64_t N = p.n_reads;
+  const int64_t N = p.read_end - p.read_begin, R0 = p.read_begin;
   if (ref_fa) {
     FILE* f = fopen(ref_fa, "w"); if (!f) return -1;
     fputs(">tig00000001 len=", f); fprintf(f, "%lld\n", (long long)p.n);
@@ -386,7 +397,7 @@ int mpc_synth_write_files(void* hv, const char* ref_fa, const char* reads_fa, co
       full += q;
       full.append(S0.down.data() + S0.down_off[(size_t)r], (size_t)(S0.down_off[(size_t)r + 1] - S0.down_off[(size_t)r]));
       if (S0.strand[(size_t)r] == '-') full = revcomp(full);
-      fprintf(f, ">read_%lld\n", (long long)r);
+      fprintf(f, ">read_%lld\n", (long long)(R0 + r));
       write_wrapped(f, full, 80);
     }
     fclose(f);
@@ -399,7 +410,7 @@ int mpc_synth_write_files(void* hv, const char* ref_fa, const char* reads_fa, co
     for (int64_t r = 0; r < N; ++r) {
       size_t ri = (size_t)r;
       fprintf(f, "read_%lld\t%lld\t%lld\t%lld\t%c\t%s\t%lld\t%lld\t%lld\t%lld\t%lld\t60\ttp:A:P\tcs:",
-              (long long)r, (long long)h->qlen[ri], (long long)h->qs[ri], (long long)h->qe[ri],
+              (long long)(R0 + r), (long long)h->qlen[ri], (long long)h->qs[ri], (long long)h->qe[ri],
               S_.strand[ri], s ? "tig00000001_revcomp" : "tig00000001", (long long)p.n,
               (long long)S_.tstart[ri], (long long)S_.tend[ri], (long long)S_.nmatch[ri],
               (long long)S_.blen[ri]);

@@ -8,17 +8,20 @@ mapped_paf_read_parser.py:37-72, driven in PAF first-occurrence order :292).
 Everything else is an order-free integer tally.  See SURVEY.md 8(e).
 
 Every shard runs the phases of include/mpc.h on its own reads.  Between the
-phases it exchanges small arrays (no read data moves):
+phases it exchanges small per-gap / per-run arrays (no read data moves), four
+collectives per step:
 
-    after parse     OR   hasleft bitmap           (which gaps hold LEFT events)
-                    SUM  diff, sub                (depth / substitution tallies)
-    after index     GATHER per-gap mixed RIGHT counts -> global run index space
-                    MAX  maxR                     (RIGHT-only gaps)
-    after tally     MAX  M per run                (longest LEFT string per run)
-                    MAX  runR per run             (length of the RIGHT string closing the run)
-    after rows      SUM  rows                     (odd rows from shard 0, slot tallies from all)
+    after parse     OR      hasleft bitmap        (which gaps hold LEFT events)
+    after index     GATHER  per-gap mixed RIGHT counts -> global run index space
+    after tally     MAX     over the workspace span MAXR | M | RUN_R
+                            (longest RIGHT string at RIGHT-only gaps, longest
+                            LEFT string per run, RIGHT string closing each run)
+    after rows      SUM     rows                  (every shard's rows hold its own
+                            reads' counts, odd positions included)
 
-after which layout and consensus are identical on every shard.  The protocol
+The depth difference array and the substitution tallies are never exchanged:
+they are linear, so they reach the result through the rows SUM.  Layout and
+consensus are then identical on every shard.  The protocol
 is written once against an ``Exchange``: ``DistExchange`` is one shard per
 process over torch.distributed (RCCL over xGMI on GPUs; gloo in the CPU
 tests), ``LocalExchange`` drives several shards in one process (used by the
@@ -69,9 +72,17 @@ class DistExchange:
         self.group = group
         self.world = dist.get_world_size(group)
         self.rank = dist.get_rank(group)
+        # RCCL ("nccl") works on device tensors in place; gloo (CPU tests, the
+        # one-GPU rehearsal of N ranks) gets host copies of device tensors
+        self.host_staged = dist.get_backend(group) != "nccl"
 
     def reduce(self, ts, op):
         (t,) = ts
+        if self.host_staged and t.is_cuda:
+            h = t.cpu()
+            self.reduce([h], op)
+            t.copy_(h)
+            return
         d = self.dist
         if op == "sum":
             d.all_reduce(t, op=d.ReduceOp.SUM, group=self.group)
@@ -100,6 +111,10 @@ class DistExchange:
 
     def gather(self, ts, outs):
         (t,), (o,) = ts, outs
+        if self.host_staged and (t.is_cuda or o.is_cuda):
+            h = self._gather_rows(t.cpu())
+            o.copy_(h.view(-1))
+            return
         self._gather_rows(t, o.view(self.world, -1))
 
     def _ints(self, xs, op):

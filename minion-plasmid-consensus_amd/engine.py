@@ -12,9 +12,9 @@ import numpy as np
 
 from . import _build
 
-LIB_PATH = os.environ.get("MPC_LIB", _build.LIBMPC)  # override: experiments with library variants
+LIB_PATH = _build.LIBMPC
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED = 0, 1, 2, 3
 DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL = 1, 2, 4, 8, 16, 32
 (BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_CNT, BUF_RIGHT_CNT_ALL,
@@ -40,6 +40,19 @@ class DataError(Exception):
         super().__init__(f"{'/'.join(names)} (first offending read index {read})")
         self.flags = flags
         self.read = read
+
+
+class PlanInfo(ctypes.Structure):
+    """mpc_plan_info (include/mpc.h): the geometry the planner chose."""
+    _fields_ = [
+        ("tally_mode", ctypes.c_int32), ("parse_window", ctypes.c_int32), ("parse_waves", ctypes.c_int32),
+        ("parse_lds_bytes", ctypes.c_int32), ("parse_workgroups", ctypes.c_int32), ("pad_", ctypes.c_int32),
+        ("max_reads_per_workgroup", ctypes.c_int64), ("reads_per_workgroup_cap", ctypes.c_int64),
+        ("workspace_bytes", ctypes.c_int64),
+    ]
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad_"}
 
 
 class _Input(ctypes.Structure):
@@ -81,6 +94,7 @@ def lib():
         L.mpc_plan_bind.argtypes = [vp, vp, ctypes.c_size_t]
         L.mpc_plan_buffer.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(i64)]
         L.mpc_plan_set_input.argtypes = [vp, ctypes.POINTER(_Input)]
+        L.mpc_plan_get_info.argtypes = [vp, ctypes.POINTER(PlanInfo)]
         for f in PHASES:
             getattr(L, "mpc_" + f).argtypes = [vp, vp]
         L.mpc_consensus.argtypes = [vp, dbl, dbl, vp]
@@ -88,12 +102,43 @@ def lib():
         L.mpc_profile_kernel.argtypes = [vp, i32, vp]
         L.mpc_profile_kernel.restype = i32
         for f in ("mpc_plan_create", "mpc_plan_destroy", "mpc_plan_workspace_bytes", "mpc_plan_bind",
-                  "mpc_plan_buffer", "mpc_plan_set_input", "mpc_consensus", "mpc_run") + tuple("mpc_" + x for x in PHASES):
+                  "mpc_plan_buffer", "mpc_plan_set_input", "mpc_plan_get_info", "mpc_consensus", "mpc_run") + tuple("mpc_" + x for x in PHASES):
             getattr(L, f).restype = i32
         if L.mpc_version() != ABI_VERSION:
             raise MpcError(f"{LIB_PATH}: ABI {L.mpc_version()} != {ABI_VERSION} (rebuild)")
         _lib = L
     return _lib
+
+
+def set_library(path):
+    """Experiments only (scripts/): load a variant build of libmpc.so instead of
+    the in-tree one.  Must be called before the first lib() call."""
+    global LIB_PATH
+    if _lib is not None:
+        raise MpcError("libmpc.so is already loaded")
+    LIB_PATH = path
+
+
+def geometry(ref_lens, reads_per_sample, cs_bytes, n_reads_global=None, read_offset=0, shard=0, n_shards=1):
+    """Host-only planning (no device): the mpc_plan_info a Plan over inputs of
+    this shape would use.  Needs no GPU."""
+    ref_len = np.ascontiguousarray(ref_lens, dtype=np.int64)
+    counts = np.asarray(reads_per_sample, dtype=np.int64)
+    rb = np.ascontiguousarray(np.concatenate([[0], np.cumsum(counts)]), dtype=np.int64)
+    n = int(rb[-1])
+    inp = _Input(n_samples=len(ref_len), h_ref_len=ref_len.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
+                 h_read_begin=rb.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n_reads=n, cs_bytes=int(cs_bytes),
+                 cs_base=0, read_offset=read_offset, n_reads_global=n_reads_global or n, shard=shard,
+                 n_shards=n_shards)
+    L = lib()
+    h = ctypes.c_void_p()
+    _check(L.mpc_plan_create(ctypes.byref(inp), int((4 * ref_len + 8).sum() + 1024), ctypes.byref(h)))
+    try:
+        info = PlanInfo()
+        _check(L.mpc_plan_get_info(h, ctypes.byref(info)))
+        return info.as_dict()
+    finally:
+        L.mpc_plan_destroy(h)
 
 
 def _check(rc):
@@ -214,6 +259,11 @@ class Plan:
         if h is not None and _lib is not None:
             _lib.mpc_plan_destroy(h)
             self.h = None
+
+    def info(self):
+        info = PlanInfo()
+        _check(lib().mpc_plan_get_info(self.h, ctypes.byref(info)))
+        return info.as_dict()
 
     def buffer(self, which, dtype):
         """View of one workspace buffer (memoized: the binding never moves)."""

@@ -63,6 +63,9 @@ def main(argv=None):
     ingest, engine, writers = pkg.ingest, pkg.engine, pkg.writers
     print("=======================================================")
     print("Python version: {}".format(sys.version))
+    print("Python environment: {}".format(sys.prefix))
+    print("Server: {}".format(os.uname()[1]))
+    print("Current directory: {}".format(os.getcwd()))
     print("Command: {}".format(" ".join(sys.argv)))
     print("Time: {}".format(time.strftime("%Y/%m/%d %T")))
     print("Engine: libmpc (HIP, gfx950)")

@@ -24,6 +24,7 @@ class _Params(ctypes.Structure):
         ("flank_min", ctypes.c_int32), ("flank_max", ctypes.c_int32),
         ("frac_partial", ctypes.c_double), ("frac_minus", ctypes.c_double),
         ("seed", ctypes.c_uint64), ("antisense", ctypes.c_int32), ("n_threads", ctypes.c_int32),
+        ("read_begin", ctypes.c_int64), ("read_end", ctypes.c_int64),
     ]
 
 
@@ -62,14 +63,16 @@ class Synth:
     inputs exactly as the host ingest produces them from the written files."""
 
     def __init__(self, n, n_reads, profile="default", seed=1, antisense=True, frac_partial=0.02,
-                 frac_minus=0.5, ins_len=(1, 3), del_len=(1, 3), flank=(0, 40), n_threads=0, **over):
+                 frac_minus=0.5, ins_len=(1, 3), del_len=(1, 3), flank=(0, 40), n_threads=0, reads=None, **over):
+        """``reads=(a, b)``: only reads [a, b) of the ``n_reads``-read set, each
+        identical to the same read of the full set (multi-GPU shards)."""
         pr = dict(PROFILES[profile])
         pr.update(over)
         p = _Params(n=n, n_reads=n_reads, p_sub=pr["p_sub"], p_ins=pr["p_ins"], p_del=pr["p_del"],
                     ins_min=ins_len[0], ins_max=ins_len[1], del_min=del_len[0], del_max=del_len[1],
                     flank_min=flank[0], flank_max=flank[1], frac_partial=frac_partial,
                     frac_minus=frac_minus, seed=seed, antisense=1 if antisense else 0,
-                    n_threads=n_threads)
+                    n_threads=n_threads, read_begin=reads[0] if reads else 0, read_end=reads[1] if reads else 0)
         self.params = p
         self.n_samples = 2 if antisense else 1
         self._h = lib().mpc_synth_new(ctypes.byref(p))

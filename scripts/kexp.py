@@ -10,6 +10,7 @@ import numpy as np, torch
 sys.path.insert(0, %r)
 pkg = importlib.import_module("minion-plasmid-consensus_amd")
 eng = pkg.engine
+eng.set_library(os.environ["KEXP_LIB"])  # variant build under test (experiments only)
 cfg = os.environ.get("KEXP_CFG", "c2")
 n, reads, prof, seed, anti = {"c2": (2686, 100000, "default", 2, True), "c4": (10000, 100000, "indel", 4, True),
                               "c3": (10000, 125000, "default", 3, False)}[cfg]
@@ -23,18 +24,11 @@ st = torch.cuda.current_stream()
 for name, k in (("parse", eng.K_PARSE), ("left", eng.K_LEFT), ("ins", eng.K_INS), ("flank", eng.K_FLANK)):
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(10)]
     for a, b in ev:
+        if k == eng.K_INS:  # K_ins consumes the run tallies: refill them first (untimed)
+            r.plan.profile_kernel(eng.K_LEFT)
         a.record(st); r.plan.profile_kernel(k); b.record(st)
     torch.cuda.synchronize()
     out[name] = float(np.median([a.elapsed_time(b) for a, b in ev])) * 1e3
-import ctypes
-L = eng.lib()
-if hasattr(L, "mpc_prof_parse"):
-    buf = (ctypes.c_ulonglong * 16)()
-    L.mpc_prof_parse(buf, 1)
-    r.plan.profile_kernel(eng.K_PARSE); torch.cuda.synchronize()
-    L.mpc_prof_parse(buf, 1)
-    v = list(buf)[:8]
-    out["prof"] = dict(zip(["stage", "toklist", "rounds", "carry", "windows", "rounds_n", "total"], v[:7]))
 st = r.plan.status()
 out["status"] = [int(x) for x in st]
 t0 = time.perf_counter()
@@ -45,7 +39,7 @@ r.step(0.1, 5.0); r.check()
 print("KEXP", json.dumps(out))
 ''' % REPO
 for lib in sys.argv[1:]:
-    env = dict(os.environ, MPC_LIB=os.path.abspath(lib))
+    env = dict(os.environ, KEXP_LIB=os.path.abspath(lib))
     p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     line = [l for l in p.stdout.splitlines() if l.startswith("KEXP")]
     print(os.path.basename(lib), line[0][5:] if line else ("FAILED rc=%d %s" % (p.returncode, p.stderr[-800:])), flush=True)

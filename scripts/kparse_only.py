@@ -11,6 +11,7 @@ import numpy as np, torch
 sys.path.insert(0, %r)
 pkg = importlib.import_module("minion-plasmid-consensus_amd")
 eng = pkg.engine
+eng.set_library(os.environ["KEXP_LIB"])  # variant build under test (experiments only)
 cfg = os.environ.get("KEXP_CFG", "c2")
 n, reads, prof, seed, anti = {"c2": (2686, 100000, "default", 2, True), "c4": (10000, 100000, "indel", 4, True),
                               "c3": (10000, 125000, "default", 3, False)}[cfg]
@@ -27,7 +28,7 @@ torch.cuda.synchronize()
 print("KP %%.1f" %% float(np.median([a.elapsed_time(b) for a, b in ev]) * 1e3), [int(x) for x in plan.status()][:4])
 ''' % REPO
 for lib in sys.argv[1:]:
-    env = dict(os.environ, MPC_LIB=os.path.abspath(lib))
+    env = dict(os.environ, KEXP_LIB=os.path.abspath(lib))
     p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
     line = [l for l in p.stdout.splitlines() if l.startswith("KP")]
     print(os.path.basename(lib), line[0][3:] if line else ("FAILED rc=%d %s" % (p.returncode, p.stderr[-800:])), flush=True)

@@ -1,0 +1,148 @@
+#!/usr/bin/env python3
+"""Time the REFERENCE script on the BASELINE configs (build container only) and
+keep its outputs as depth golden fixtures.
+
+    python3 scripts/time_reference.py [--ref-script PATH] [--core 0] [--only c2_10pct ...]
+
+For every case the inputs are written by the build's seeded generator
+(csrc/synth.cpp), as a read-index slice of the very read set bench.py uses for
+that config (Synth(reads=(a, b)) yields reads a..b-1 of the full set, bit for
+bit).  The reference runs once per strand, as the Snakemake rule does
+(Snakefile:401-423), pinned to one core (`taskset -c`), with ``python3 -B`` so
+nothing is written into the read-only reference tree; its wall time is taken
+around the subprocess.  SURVEY.md §8(d): the reference is single-threaded and
+its rate is flat in the number of reads, so configs that are impractical in
+Python at full size are timed on a seeded subsample and extrapolated linearly
+(labelled "extrapolated").
+
+Outputs
+  profiles/ref_cpu_baseline.json   per config: aligned bases/s, wall, sample, CPU model, cores
+  tests/golden_depth/<case>/       the reference's three output files per strand and
+                                   (mdf, gtf) run + the generator parameters (case.json);
+                                   inputs are NOT stored: tests regenerate them
+"""
+import argparse
+import gzip
+import json
+import os
+import platform
+import shutil
+import subprocess
+import sys
+import tempfile
+import time
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+import importlib  # noqa: E402
+
+synth = importlib.import_module("minion-plasmid-consensus_amd.synth")
+
+GOLDEN = os.path.join(REPO, "tests", "golden_depth")
+RECORD = os.path.join(REPO, "profiles", "ref_cpu_baseline.json")
+
+# case: (bench config, synth kwargs, reads slice, full reads per sample, strands, (mdf, gtf) runs)
+CASES = {
+    "c1_full": ("c1", dict(n=5000, n_reads=20_000, profile="default", seed=1, antisense=False), (0, 20_000), 20_000,
+                1, [(0.1, 5.0)]),
+    "c2_10pct": ("c2", dict(n=2686, n_reads=100_000, profile="default", seed=2, antisense=True), (0, 10_000), 100_000,
+                 2, [(0.1, 5.0), (-1.0, 1.0)]),
+    "c3_1pct": ("c3", dict(n=10_000, n_reads=1_000_000, profile="default", seed=3, antisense=False), (0, 10_000),
+                1_000_000, 1, [(0.1, 5.0)]),
+    "c4_5pct": ("c4", dict(n=10_000, n_reads=100_000, profile="indel", seed=4, antisense=True), (0, 5_000), 100_000,
+                2, [(0.1, 5.0)]),
+    "c5_p0_10pct": ("c5", dict(n=30_000, n_reads=10_000, profile="default", seed=5000, antisense=True), (0, 1_000),
+                    10_000, 2, [(0.1, 5.0)]),
+}
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return platform.processor() or "unknown"
+
+
+def wgz(path, data):
+    with open(path, "wb") as raw:
+        with gzip.GzipFile(fileobj=raw, mode="wb", compresslevel=9, mtime=0, filename="") as f:
+            f.write(data)
+
+
+def run_case(name, script, core):
+    cfg, kw, (a, b), full, strands, runs = CASES[name]
+    syn = synth.Synth(reads=(a, b), **kw)
+    aligned = int(sum(int(syn.sample(s)["aligned"].sum()) for s in range(strands)))
+    cdir = os.path.join(GOLDEN, name)
+    if os.path.exists(cdir):
+        shutil.rmtree(cdir)
+    os.makedirs(cdir)
+    manifest = {"config": cfg, "synth": kw, "reads": [a, b], "strands": strands, "runs": []}
+    walls = []
+    with tempfile.TemporaryDirectory() as tmp:
+        p = lambda f: os.path.join(tmp, f)
+        syn.write_files(p("ref.fa"), p("reads.fa"), p("s0.paf"), p("ref1.fa") if strands > 1 else None,
+                        p("s1.paf") if strands > 1 else None)
+        env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+        for k, (mdf, gtf) in enumerate(runs):
+            ent = {"mdf": mdf, "gtf": gtf, "strands": []}
+            for s in range(strands):
+                ref = p("ref.fa") if s == 0 else p("ref1.fa")
+                cmd = ["taskset", "-c", str(core), sys.executable, "-B", script, "--ref", ref, "--reads", p("reads.fa"),
+                       "--paf", p(f"s{s}.paf"), "--consensus", p("c.fa"), "--chromat", p("ch.tsv"),
+                       "--accuracies", p("acc.tsv"), "--min_depth_factor", repr(mdf),
+                       "--global_threshold_factor", repr(gtf)]
+                t0 = time.perf_counter()
+                r = subprocess.run(cmd, env=env, capture_output=True, text=True)
+                wall = time.perf_counter() - t0
+                if r.returncode != 0:
+                    raise SystemExit(f"{name}: reference exit {r.returncode}: {r.stderr[-400:]}")
+                if k == 0:
+                    walls.append(wall)
+                files = {}
+                for f in ("c.fa", "ch.tsv", "acc.tsv"):
+                    fn = f"run{k}_s{s}_{f}.gz"
+                    wgz(os.path.join(cdir, fn), open(p(f), "rb").read())
+                    files[f] = fn
+                ent["strands"].append({"files": files, "wall_s": round(wall, 3)})
+                print(f"{name} run{k} strand{s}: {wall:.2f} s", flush=True)
+            manifest["runs"].append(ent)
+    with open(os.path.join(cdir, "case.json"), "w") as f:
+        json.dump(manifest, f, indent=1, sort_keys=True)
+    wall = sum(walls)
+    frac = (b - a) / full
+    return cfg, {
+        "value": aligned / wall, "unit": "aligned bases/s", "cores": 1, "kind": "reference",
+        "wall_s": round(wall, 3), "aligned_bases": aligned, "strand_jobs": strands,
+        "extrapolated": frac < 1.0,
+        "sample": (f"{name}: reads [{a}, {b}) of the {full}-read {cfg} set ({100 * frac:g} %), "
+                   f"{strands} strand job(s) run one after the other (Snakefile:401-423), "
+                   f"/root/reference/src/mapped_paf_read_parser.py whole script, taskset -c {core}"
+                   + ("; rate extrapolated linearly to the full set (SURVEY §8(d))" if frac < 1.0 else "")),
+    }
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--ref-script", default="/root/reference/src/mapped_paf_read_parser.py")
+    ap.add_argument("--core", type=int, default=0)
+    ap.add_argument("--only", nargs="*")
+    a = ap.parse_args()
+    os.makedirs(GOLDEN, exist_ok=True)
+    rec = json.load(open(RECORD)) if os.path.exists(RECORD) else {}
+    rec["host"] = {"cpu_model": cpu_model(), "logical_cpus": os.cpu_count(), "python": platform.python_version(),
+                   "where": "build container (the reference does not exist on the GPU box)"}
+    rec.setdefault("configs", {})
+    for name in a.only or CASES:
+        cfg, r = run_case(name, a.ref_script, a.core)
+        rec["configs"][cfg] = r
+        with open(RECORD, "w") as f:
+            json.dump(rec, f, indent=1, sort_keys=True)
+        print(json.dumps({cfg: r}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -25,7 +25,7 @@ def test_library_exports_all(pkg):
     for name in declared():
         assert hasattr(lib, name), name
     lib.mpc_version.restype = ctypes.c_int
-    assert lib.mpc_version() == pkg.engine.ABI_VERSION == 4
+    assert lib.mpc_version() == pkg.engine.ABI_VERSION == 5
 
 
 def test_no_oracle_in_product():
@@ -45,3 +45,22 @@ def test_ingest_library_exports_all(pkg):
     assert "mpc_ingest" in names and "mpc_ingest_free" in names
     for name in names:
         assert hasattr(lib, name), name
+
+
+def test_planner_geometry(pkg):
+    """Host-only planning (no device work): which K_parse tally mode every
+    BASELINE config runs in, and the reads-per-workgroup cap that keeps the
+    16-bit LDS tallies exact (mpc_kernels.hip wg_reads_cap)."""
+    g = pkg.engine.geometry
+    c2 = g([2686, 2686], [100_000, 100_000], 63 << 20)
+    assert c2["tally_mode"] == 1 and c2["max_reads_per_workgroup"] <= c2["reads_per_workgroup_cap"] == 32767
+    c3 = g([10_000], [1_000_000], 1200 << 20)
+    assert c3["tally_mode"] == 2 and c3["max_reads_per_workgroup"] <= c3["reads_per_workgroup_cap"] == 16383
+    c5 = g([30_000] * 24, [10_000] * 24, 24 * 3600 * 10_000 // 100)
+    assert c5["tally_mode"] in (2, 3)
+    # the cap binds: 4.9 M tiny reads beside one 10 kb sample put 16383 reads in a workgroup
+    st = g([10_000, 30], [100, 16383 * 300], 16383 * 300 * 12)
+    assert st["tally_mode"] == 2
+    assert st["max_reads_per_workgroup"] == st["reads_per_workgroup_cap"] == 16383
+    for info in (c2, c3, c5, st):
+        assert info["parse_lds_bytes"] <= 160 * 1024 and info["parse_waves"] in (8, 12, 16)

@@ -1,0 +1,90 @@
+"""The multi-GPU protocol with REAL HIP plans across processes.
+
+Two / three fresh processes share cuda:0 (RCCL needs one GPU per rank, so the
+ranks exchange over gloo with host-staged tensors: dist.DistExchange), each
+generates only its contiguous slice of one global read set (Synth(reads=...),
+exactly as bench.py --gpus N does), runs ShardedPileup over its own plan, and
+returns its fetched calls.  Every rank must hold the single-pileup result of
+the whole read set, bit-exact with the C oracle -- including the order-dependent
+slot layout at gaps with both LEFT and RIGHT events
+(mapped_paf_read_parser.py:37-72 in the read order of :292).
+"""
+import importlib
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+import depth_util as du
+
+pytestmark = pytest.mark.gpu
+
+SPECS = {
+    "c2like": dict(n=2686, n_reads=24_000, profile="default", seed=2, frac_partial=0.05),
+    "partial_indel": dict(n=900, n_reads=6_000, profile="indel", seed=71, frac_partial=0.5, flank=(0, 60),
+                          ins_len=(1, 8), del_len=(1, 6)),
+}
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, spec_name, q):
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(0)
+        tdist.init_process_group("gloo", rank=rank, world_size=world)
+        try:
+            pkg = importlib.import_module("minion-plasmid-consensus_amd")
+            dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
+            spec = SPECS[spec_name]
+            n = spec["n_reads"]
+            a, b = n * rank // world, n * (rank + 1) // world
+            syn = pkg.synth.Synth(reads=(a, b), **spec)
+            samples = [syn.sample(0), syn.sample(1)]
+            sp = dmod.ShardedPileup([samples], [0], ex=dmod.DistExchange())
+            out = []
+            for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
+                sp.step(mdf, gtf)
+                sp.check()
+                out.append([{k: v for k, v in r.items()} for r in sp.fetch()])
+            q.put((rank, out, None))
+        finally:
+            tdist.destroy_process_group()
+    except Exception as e:  # reported to the parent
+        q.put((rank, None, repr(e)))
+
+
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("spec_name,world", [("c2like", 2), ("partial_indel", 3)])
+def test_dist_exchange_real_plans(pkg, spec_name, world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, spec_name, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        res = sorted((q.get(timeout=240) for _ in range(world)), key=lambda x: x[0])
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.is_alive():
+                p.kill()
+    for rank, _, err in res:
+        assert err is None, (rank, err)
+    for p in procs:
+        assert p.exitcode == 0
+    syn = pkg.synth.Synth(**SPECS[spec_name])
+    samples = [syn.sample(0), syn.sample(1)]
+    full = du.oracle_many(samples, -1.0, 1.0)
+    for rank, out, _ in res:
+        for (mdf, gtf), got in zip(((-1.0, 1.0), (0.1, 5.0)), out):
+            for s, (g, f) in enumerate(zip(got, full)):
+                du.compare(g, du.derive(f, mdf, gtf), (spec_name, world, rank, s, mdf))

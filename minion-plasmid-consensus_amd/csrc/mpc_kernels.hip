@@ -389,6 +389,132 @@ __device__ __forceinline__ void chunk_store(uint8_t* p, U8x32 v) {
   reinterpret_cast<uint4*>(p)[1] = v.b;
 }
 
+// End of a parse workgroup: flush the LDS position
+// tallies and the LEFT-gap bitmap with contiguous atomics, then bucket-sort the
+// workgroup's insertion events by gap (counting sort, kBW gaps per bucket) from
+// its event regions (nreg regions: count wcnt[k] at ins_raw[wbase[k]]) into
+// ins_sorted, staging chunks of stg_cap events in LDS at stg.  Every thread of
+// the block calls it.
+template <int TM>
+__device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, int64_t r0, uint32_t* hl,
+                               const uint32_t* bcnt, uint32_t* uni, const uint32_t* wcnt, const int64_t* wbase,
+                               int nreg, uint64_t* stg, int stg_cap) {
+  constexpr bool fused = TM != 0;
+  constexpr bool lds_sub = TM == 1 || TM == 2;
+  constexpr bool packed = TM >= 2;
+  const int l = lane();
+  const int nsub = lds_sub ? 2 * (n + 1) : 0;
+  const uint32_t* sub_l = uni;
+  const uint32_t* del_l = uni + nsub;
+  // ---- flush LDS tallies and the LEFT-gap bitmap ----
+  if (fused) {
+    // one word per lane, consecutive lanes on consecutive words: a wave's
+    // atomics cover contiguous bytes (memory-side atomics run at full rate
+    // only on contiguous segments)
+    for (int p = threadIdx.x; p <= n; p += blockDim.x) {
+      int32_t dv;
+      if (packed) dv = (int32_t)((del_l[p >> 1] >> (16 * (p & 1))) & 0xffffu) - 0x8000;
+      else { const uint32_t dl = del_l[p]; dv = (int32_t)(dl >> 16) - (int32_t)(dl & 0xffffu); }
+      if (dv) atomicAdd(a.diff + gb + p, dv);
+    }
+    uint32_t* sg = a.sub + (int64_t)gb * 4;
+    for (int k = threadIdx.x; lds_sub && k < 4 * (n + 1); k += blockDim.x) {  // word k = position k/4, code k%4
+      const uint32_t w2 = sub_l[2 * (k >> 2) + ((k >> 1) & 1)];
+      const uint32_t v = (k & 1) ? (w2 >> 16) : (w2 & 0xffffu);
+      if (v) atomicAdd(sg + k, v);
+    }
+  }
+  for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) {
+    const uint32_t v = hl[k];
+    if (!v) continue;
+    const int g0 = gb + 32 * k;  // global bit of local bit 0 of this word
+    atomicOr(a.hasleft + (g0 >> 5), v << (g0 & 31));
+    if (g0 & 31) atomicOr(a.hasleft + (g0 >> 5) + 1, v >> (32 - (g0 & 31)));
+  }
+  __syncthreads();
+  // ---- bucket-sort this workgroup's insertion events by gap (counting sort) ----
+  // bucket counts: bcnt (main loop); cursors and the scatter's chunk tables alias the flushed tallies
+  uint32_t* bcur = uni;
+  const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;
+  const int bstride = (int)blockDim.x;
+  constexpr int kEpiU = 8;  // events per thread per staged scatter chunk
+  if (threadIdx.x < 64) {  // exclusive scan over buckets by one wave
+    int carry_b = 0;
+    for (int c0 = 0; c0 < nbk; c0 += 64) {
+      const int k = c0 + l;
+      const int v = k < nbk ? (int)bcnt[k] : 0;
+      const int inc = wave_scan_i32(v);
+      if (k < nbk) {
+        bcur[k] = (uint32_t)(carry_b + inc - v);
+        a.bk_cnt[(int64_t)blockIdx.x * a.nbs + k] = v;
+        a.bk_off[(int64_t)blockIdx.x * a.nbs + k] = carry_b + inc - v;
+      }
+      carry_b += wave_last_i32(inc);
+    }
+  }
+  if (threadIdx.x == 0) a.rbase[blockIdx.x] = rb_wg;
+  __syncthreads();
+  // scatter, staged: chunks of the workgroup's events (the wave regions
+  // concatenated) are counting-sorted by bucket in LDS (the per-wave areas are
+  // free now), then written out so that consecutive lanes store consecutive
+  // addresses of a bucket's run (8-byte scattered stores left most 128-byte
+  // lines partially written: ~8x HBM write amplification at C4)
+  uint64_t* dst = a.ins_sorted + rb_wg;
+  uint32_t* ccnt = bcur + nbk;  // [nbk] per-chunk bucket counts
+  uint32_t* coff = ccnt + nbk;  // [nbk + 1] their exclusive scan (coff[nbk]: events staged)
+  const int chunk = min(stg_cap, kEpiU * bstride);
+  for (int k = threadIdx.x; k < nbk; k += bstride) ccnt[k] = 0;
+  int Ev = 0;
+  for (int ww = 0; ww < nreg; ++ww) Ev += (int)wcnt[ww];
+  int ww_t = 0, pre_t = 0;  // this thread's walk over the regions (its k only grow)
+  __syncthreads();
+  for (int c0 = 0; c0 < Ev; c0 += chunk) {
+    const int c1 = min(c0 + chunk, Ev);
+    uint64_t ev[kEpiU];
+    uint32_t rk[kEpiU];
+#pragma unroll
+    for (int u = 0; u < kEpiU; ++u) {
+      const int k = c0 + (int)threadIdx.x + u * bstride;
+      ev[u] = ~0ull;
+      if (k < c1) {
+        while (k >= pre_t + (int)wcnt[ww_t]) { pre_t += (int)wcnt[ww_t]; ++ww_t; }
+        ev[u] = a.ins_raw[wbase[ww_t] + (k - pre_t)];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < kEpiU; ++u) {
+      const uint32_t gap = (uint32_t)(ev[u] >> 10) & kNullGap;
+      rk[u] = gap <= (uint32_t)n ? atomicAdd(ccnt + gap / kBW, 1u) : ~0u;
+    }
+    __syncthreads();
+    if (threadIdx.x < 64) {
+      int cb = 0;
+      for (int b0 = 0; b0 < nbk; b0 += 64) {
+        const int k = b0 + l;
+        const int v = k < nbk ? (int)ccnt[k] : 0;
+        const int inc = wave_scan_i32(v);
+        if (k < nbk) coff[k] = (uint32_t)(cb + inc - v);
+        cb += wave_last_i32(inc);
+      }
+      if (l == 0) coff[nbk] = (uint32_t)cb;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int u = 0; u < kEpiU; ++u)
+      if (rk[u] != ~0u) stg[coff[((uint32_t)(ev[u] >> 10) & kNullGap) / kBW] + rk[u]] = ev[u];
+    __syncthreads();
+    const int staged = (int)coff[nbk];
+    for (int j = threadIdx.x; j < staged; j += bstride) {
+      const uint64_t e = stg[j];
+      const int b = (int)(((uint32_t)(e >> 10) & kNullGap) / kBW);
+      dst[bcur[b] + (j - (int)coff[b])] = e;
+    }
+    __syncthreads();
+    for (int k = threadIdx.x; k < nbk; k += bstride) { bcur[k] += ccnt[k]; ccnt[k] = 0; }
+    __syncthreads();
+  }
+}
+
 // Workgroup = contiguous reads of ONE sample (host work table); wave w takes
 // the w-th part of them and streams their cs bytes in windows of WIN bytes
 // (WIN/64 per lane, coalesced; the next window is loaded while this one is
@@ -781,118 +907,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   }
   if (l == 0) { wcnt[w] = nev; wbase[w] = ev_base; }
   __syncthreads();
-  // ---- flush LDS tallies and the LEFT-gap bitmap ----
-  if (fused) {
-    // one word per lane, consecutive lanes on consecutive words: a wave's
-    // atomics cover contiguous bytes (memory-side atomics run at full rate
-    // only on contiguous segments)
-    for (int p = threadIdx.x; p <= n; p += blockDim.x) {
-      int32_t dv;
-      if (packed) dv = (int32_t)((del_l[p >> 1] >> (16 * (p & 1))) & 0xffffu) - 0x8000;
-      else { const uint32_t dl = del_l[p]; dv = (int32_t)(dl >> 16) - (int32_t)(dl & 0xffffu); }
-      if (dv) atomicAdd(a.diff + gb + p, dv);
-    }
-    uint32_t* sg = a.sub + (int64_t)gb * 4;
-    for (int k = threadIdx.x; lds_sub && k < 4 * (n + 1); k += blockDim.x) {  // word k = position k/4, code k%4
-      const uint32_t w2 = sub_l[2 * (k >> 2) + ((k >> 1) & 1)];
-      const uint32_t v = (k & 1) ? (w2 >> 16) : (w2 & 0xffffu);
-      if (v) atomicAdd(sg + k, v);
-    }
-  }
-  for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) {
-    const uint32_t v = hl[k];
-    if (!v) continue;
-    const int g0 = gb + 32 * k;  // global bit of local bit 0 of this word
-    atomicOr(a.hasleft + (g0 >> 5), v << (g0 & 31));
-    if (g0 & 31) atomicOr(a.hasleft + (g0 >> 5) + 1, v >> (32 - (g0 & 31)));
-  }
-  __syncthreads();
-  // ---- bucket-sort this workgroup's insertion events by gap (counting sort) ----
-  // bucket counts: bcnt (main loop); cursors and the scatter's chunk tables alias the flushed tallies
-  uint32_t* bcur = uni;
-  const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;
-  const int bstride = (int)blockDim.x;
-#ifndef MPC_EPIU
-#define MPC_EPIU 8
-#endif
-  constexpr int kEpiU = MPC_EPIU;  // events per thread per staged scatter chunk
-  if (threadIdx.x < 64) {  // exclusive scan over buckets by one wave
-    int carry_b = 0;
-    for (int c0 = 0; c0 < nbk; c0 += 64) {
-      const int k = c0 + l;
-      const int v = k < nbk ? (int)bcnt[k] : 0;
-      const int inc = wave_scan_i32(v);
-      if (k < nbk) {
-        bcur[k] = (uint32_t)(carry_b + inc - v);
-        a.bk_cnt[(int64_t)blockIdx.x * a.nbs + k] = v;
-        a.bk_off[(int64_t)blockIdx.x * a.nbs + k] = carry_b + inc - v;
-      }
-      carry_b += wave_last_i32(inc);
-    }
-  }
-  if (threadIdx.x == 0) a.rbase[blockIdx.x] = rb_wg;
-  __syncthreads();
-  // scatter, staged: chunks of the workgroup's events (the wave regions
-  // concatenated) are counting-sorted by bucket in LDS (the per-wave areas are
-  // free now), then written out so that consecutive lanes store consecutive
-  // addresses of a bucket's run (8-byte scattered stores left most 128-byte
-  // lines partially written: ~8x HBM write amplification at C4)
-  uint64_t* dst = a.ins_sorted + rb_wg;
-  uint32_t* ccnt = bcur + nbk;  // [nbk] per-chunk bucket counts
-  uint32_t* coff = ccnt + nbk;  // [nbk + 1] their exclusive scan (coff[nbk]: events staged)
-  uint64_t* stg = reinterpret_cast<uint64_t*>(lds);
-  const int chunk = min(nw * (int)sizeof(WL) / 8, kEpiU * bstride);
-  for (int k = threadIdx.x; k < nbk; k += bstride) ccnt[k] = 0;
-  int Ev = 0;
-  for (int ww = 0; ww < nw; ++ww) Ev += (int)wcnt[ww];
-  int ww_t = 0, pre_t = 0;  // this thread's walk over the regions (its k only grow)
-  __syncthreads();
-  for (int c0 = 0; c0 < Ev; c0 += chunk) {
-    const int c1 = min(c0 + chunk, Ev);
-    uint64_t ev[kEpiU];
-    uint32_t rk[kEpiU];
-#pragma unroll
-    for (int u = 0; u < kEpiU; ++u) {
-      const int k = c0 + (int)threadIdx.x + u * bstride;
-      ev[u] = ~0ull;
-      if (k < c1) {
-        while (k >= pre_t + (int)wcnt[ww_t]) { pre_t += (int)wcnt[ww_t]; ++ww_t; }
-        ev[u] = a.ins_raw[wbase[ww_t] + (k - pre_t)];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kEpiU; ++u) {
-      const uint32_t gap = (uint32_t)(ev[u] >> 10) & kNullGap;
-      rk[u] = gap <= (uint32_t)n ? atomicAdd(ccnt + gap / kBW, 1u) : ~0u;
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-      int cb = 0;
-      for (int b0 = 0; b0 < nbk; b0 += 64) {
-        const int k = b0 + l;
-        const int v = k < nbk ? (int)ccnt[k] : 0;
-        const int inc = wave_scan_i32(v);
-        if (k < nbk) coff[k] = (uint32_t)(cb + inc - v);
-        cb += wave_last_i32(inc);
-      }
-      if (l == 0) coff[nbk] = (uint32_t)cb;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kEpiU; ++u)
-      if (rk[u] != ~0u) stg[coff[((uint32_t)(ev[u] >> 10) & kNullGap) / kBW] + rk[u]] = ev[u];
-    __syncthreads();
-    const int staged = (int)coff[nbk];
-    for (int j = threadIdx.x; j < staged; j += bstride) {
-      const uint64_t e = stg[j];
-      const int b = (int)(((uint32_t)(e >> 10) & kNullGap) / kBW);
-      dst[bcur[b] + (j - (int)coff[b])] = e;
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < nbk; k += bstride) { bcur[k] += ccnt[k]; ccnt[k] = 0; }
-    __syncthreads();
-  }
+  parse_epilogue<TM>(a, n, gb, nbk, r0, hl, bcnt, uni, wcnt, wbase, nw, reinterpret_cast<uint64_t*>(lds),
+                     nw * (int)sizeof(WL) / 8);
 }
+
 
 // ---------------------------------------------------------------------------
 // Downstream (RIGHT) events.  A gap holding only RIGHT events needs only its
@@ -2435,7 +2453,8 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WPARSE), p->work_parse.data(), 4 * p->work_parse.size(), hipMemcpyHostToDevice));
   if (!p->work_bc.empty())
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WBC), p->work_bc.data(), 4 * p->work_bc.size(), hipMemcpyHostToDevice));
-  HIPCHK(hipFuncSetAttribute(parse_kernel(p->tally_mode, p->parse_win), hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
+  HIPCHK(hipFuncSetAttribute(parse_kernel(p->tally_mode, p->parse_win), hipFuncAttributeMaxDynamicSharedMemorySize,
+                             p->parse_lds));
   p->bound = true;
   p->runt_dirty = true;
   return MPC_OK;

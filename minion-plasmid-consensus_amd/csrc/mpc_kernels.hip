@@ -1196,6 +1196,7 @@ __device__ __forceinline__ int64_t run_left(const int32_t* rs, const int32_t* rs
 #define MPC_EPT 16
 #endif
 constexpr int kUB = MPC_UB;           // threads of the unit kernels (K_left, K_ins)
+constexpr int kLeftVals = 4096;       // mixed RIGHT reads of a bucket staged in K_left's LDS
 constexpr int kEPT = MPC_EPT;         // events per thread per unit (loads batched)
 constexpr int kUnit = kUB * kEPT;     // events per work unit
 
@@ -1363,17 +1364,21 @@ struct LeftArgs {
 __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
   __shared__ int64_t s_key;
   __shared__ int32_t s_val;
-  __shared__ uint32_t Ml[kBW][kKMax];
+  // strides padded to odd word counts: every gap of the bucket starts on a
+  // different bank (unpadded, all gaps' run-0 counters shared 16 banks)
+  constexpr int kMs = kKMax + 1, kTs = kKMax * 16 + 1;
+  __shared__ uint32_t Ml[kBW * kMs];
   __shared__ int32_t s_pre[256];
   __shared__ int64_t s_src[256];
   __shared__ int32_t s_wsum[4];
   __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1];  // per gap of the bucket (K_left)
-  __shared__ uint32_t Tl[kBW][kKMax][16];  // per (gap, run): inline bases [bi from the 3' end][code]
+  __shared__ uint32_t Tl[kBW * kTs];  // per (gap, run): inline bases [bi from the 3' end][code]
+  __shared__ int32_t s_vals[kLeftVals];   // the bucket's mixed RIGHT reads (vals_out), searched per event
   // (K_units raises DE_INTERNAL instead of overrunning the unit list)
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
-    for (int k = threadIdx.x; k < kBW * kKMax; k += blockDim.x) (&Ml[0][0])[k] = 0;
-    for (int k = threadIdx.x; k < kBW * kKMax * 16; k += blockDim.x) (&Tl[0][0][0])[k] = 0;
+    for (int k = threadIdx.x; k < kBW * kMs; k += blockDim.x) Ml[k] = 0;
+    for (int k = threadIdx.x; k < kBW * kTs; k += blockDim.x) Tl[k] = 0;
     const UnitView uv = load_unit<false>(a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, a.right_start, a.rsl,
                                          a.roff, nullptr, nullptr, nullptr, s_pre, s_src, s_wsum, s_rs, s_rsl, s_roff, nullptr);
     const int n = uv.n;
@@ -1385,6 +1390,13 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
       const int e = uv.e0 + (int)threadIdx.x + q * kUB;
       evs[q] = e < uv.e0 + uv.cnt ? a.ins_sorted[unit_event_src(s_pre, s_src, e)] : ~0ull;
     }
+    // the run of an event at a mixed gap is a search of the gap's RIGHT reads:
+    // stage the bucket's (contiguous in vals_out) in LDS, so no event waits on
+    // a chain of dependent global loads
+    const int32_t v0 = s_rsl[0], vn = s_rsl[uv.gl + 1 - g0] - v0;
+    const bool vl = vn <= kLeftVals;
+    for (int k = threadIdx.x; vl && k < vn; k += blockDim.x) s_vals[k] = a.vals_out[v0 + k];
+    __syncthreads();
 #pragma unroll
     for (int q = 0; q < kEPT; ++q) {
       const uint64_t ev = evs[q];
@@ -1395,12 +1407,15 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
       const int L = (int)((ev >> 8) & 3u) + 1;
       const int p = gap - g0;
       const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
-      const int64_t k = s_roff[p] + (lb > la ? lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la : 0);
+      int64_t k = s_roff[p];
+      if (lb > la) k += vl ? lower_bound_i32(s_vals, la - v0, lb - v0, (int32_t)rg) - (la - v0)
+                           : lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la;
       // the bases too, run-relative (LEFT: base bi from the 3' end lands on the
       // run's slot hi_run - 1 - bi, :37-62): K_ins maps them to rows after the layout
       if (k < kKMax) {
-        atomicMax(&Ml[p][k], (uint32_t)L);
-        for (int j = 0; j < L; ++j) atomicAdd(&Tl[p][k][4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u)], 1u);
+        atomicMax(&Ml[p * kMs + k], (uint32_t)L);
+        uint32_t* tp = Tl + p * kTs + k * 16;
+        for (int j = 0; j < L; ++j) atomicAdd(tp + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
       } else {
         atomicMax(a.M + s_rs[p] + g + k, L);
         uint32_t* rt = a.runt + (s_rs[p] + g + k) * 16;
@@ -1410,12 +1425,12 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
     __syncthreads();
     for (int q = threadIdx.x; q < kBW * kKMax; q += blockDim.x) {
       const int k = q % kKMax, p = q / kKMax;
-      const uint32_t m = Ml[p][k];
+      const uint32_t m = Ml[p * kMs + k];
       if (m) atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + k, (int32_t)m);
     }
     for (int q = threadIdx.x; q < kBW * kKMax * 16; q += blockDim.x) {  // contiguous per (gap, run)
-      const uint32_t v = (&Tl[0][0][0])[q];
       const int k = (q >> 4) % kKMax, p = (q >> 4) / kKMax;
+      const uint32_t v = Tl[p * kTs + k * 16 + (q & 15)];
       if (v) atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + k) * 16 + (q & 15), v);
     }
     __syncthreads();
@@ -1675,7 +1690,7 @@ __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
 // gap (for full-length reads: gap 0 upstream, gap n downstream -- the hot
 // gaps) are tallied in LDS windows, everything else with global atomics.
 // ---------------------------------------------------------------------------
-constexpr int kFR = 256;        // reads per block (one per thread)
+constexpr int kFR = 512;        // reads per block (one per thread): C2's 200k reads fit one round of resident blocks
 constexpr int kWinRows = 256;   // LDS window rows per flank side
 
 struct FlankArgs {
@@ -1704,15 +1719,17 @@ constexpr int kStageB = 8192;  // flank bytes staged in LDS per chunk (a block's
 // without a search: the starts of the block's non-empty flanks are bits of a
 // chunk bitmap with per-word prefix counts, so owner(x) = (starts <= x) - 1 in
 // the compacted list of non-empty flanks {start, row of byte 0}.
-__global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
-  __shared__ uint32_t win[2][kWinRows * 4];
+__global__ __launch_bounds__(kFR) void K_flank(FlankArgs a) {
+  // row r, code c at word 5 r + c: consecutive rows (the bytes of one flank,
+  // on consecutive lanes) fall on distinct banks
+  __shared__ uint32_t win[2][kWinRows * 5];
   __shared__ __attribute__((aligned(16))) uint8_t stage[kStageB + 16];
   __shared__ int32_t t_start[kFR], t_row[kFR], t_read[kFR];  // compacted non-empty flanks of the current side
   __shared__ uint32_t bm[kStageB / 32];                      // flank starts in the chunk
   __shared__ int32_t wpre[kStageB / 32];                     // starts before each bitmap word (+ chunk base)
   __shared__ int32_t s_gap[2][kFR];
   __shared__ int64_t s_w0[2];
-  __shared__ int32_t s_w[4], s_nne, s_cbase;
+  __shared__ int32_t s_w[kFR / 64], s_nne, s_cbase;
   if (a.status[MPC_ST_FLAGS] & (DE_CAP | DE_INTERNAL)) return;
   const int tid = threadIdx.x, l = lane(), w = tid >> 6;
   const int64_t r0 = (int64_t)blockIdx.x * kFR;
@@ -1729,7 +1746,7 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
     off[0] = a.up_off[r]; end[0] = a.up_off[r + 1];
     off[1] = a.down_off[r]; end[1] = a.down_off[r + 1];
   }
-  for (int k = tid; k < 2 * kWinRows * 4; k += blockDim.x) (&win[0][0])[k] = 0;
+  for (int k = tid; k < 2 * kWinRows * 5; k += blockDim.x) (&win[0][0])[k] = 0;
   int64_t rs[2] = {-1, -1};
   int32_t gap[2] = {-1, -1};
   if (live) {
@@ -1788,7 +1805,7 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
       t_row[c] = (rs[side] >= 0 && rs[side] + L <= tot) ? (int32_t)rs[side] : -1;
       t_read[c] = tid;
     }
-    if (tid == 255) s_nne = wp + inc;
+    if (tid == kFR - 1) s_nne = wp + inc;
     const int64_t w0 = s_w0[side];
     uint32_t* wn = win[side];
     for (int64_t c0 = 0; c0 < nb; c0 += kStageB) {  // chunks of the block's byte range
@@ -1837,7 +1854,7 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
         const int code = code_exact(stage[x + sh0]);
         if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
         const int64_t wr = row - w0;
-        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 4 + code, 1u);
+        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
         else atomicAdd(a.rows + row * 4 + code, 1u);
       }
     }
@@ -1846,7 +1863,7 @@ __global__ __launch_bounds__(256) void K_flank(FlankArgs a) {
   for (int side = 0; side < 2; ++side) {
     const int64_t w0 = s_w0[side];
     for (int k = tid; k < kWinRows * 4; k += blockDim.x) {
-      const uint32_t v = win[side][k];
+      const uint32_t v = win[side][(k >> 2) * 5 + (k & 3)];
       if (v) atomicAdd(a.rows + w0 * 4 + k, v);
     }
   }
@@ -2575,7 +2592,7 @@ int mpc_rows(mpc_plan* p, void* stream) {
   hipLaunchKernelGGL(K_ins, dim3(ins_grid(p)), dim3(kUB), 0, st, ins_args(p, d));
   HIPCHK(hipGetLastError());
   p->runt_dirty = false;  // K_ins (enqueued) zeroes every run tally it maps (all runs of all gaps)
-  if (p->N > 0) hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(256), 0, st, flank_args(p, d));
+  if (p->N > 0) hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(kFR), 0, st, flank_args(p, d));
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -2612,7 +2629,7 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
       hipLaunchKernelGGL(K_ins, dim3(ins_grid(p)), dim3(kUB), 0, st, ins_args(p, d));
       break;
     case MPC_K_FLANK:
-      hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(256), 0, st, flank_args(p, d));
+      hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(kFR), 0, st, flank_args(p, d));
       break;
     default:
       return fail(MPC_E_ARG, "unknown kernel");

@@ -13,7 +13,7 @@ pkg = importlib.import_module("minion-plasmid-consensus_amd")
 eng = pkg.engine
 eng.set_library(os.environ["KEXP_LIB"])  # variant build under test (experiments only)
 cfg = os.environ.get("KEXP_CFG", "c2")
-n, reads, prof, seed, anti = {"c2": (2686, 100000, "default", 2, True), "c4": (10000, 100000, "indel", 4, True),
+n, reads, prof, seed, anti = {"c2": (2686, 100000, "default", 2, True), "c4": (10000, 100000, "indel", 4, True), "c5": (30000, 10000, "default", 5000, True),
                               "c3": (10000, 125000, "default", 3, False)}[cfg]
 syn = pkg.synth.Synth(n=n, n_reads=reads, profile=prof, seed=seed, antisense=anti)
 samples = [syn.sample(s) for s in range(2 if anti else 1)]

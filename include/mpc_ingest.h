@@ -1,12 +1,14 @@
 /*
- * mpc_ingest.h -- C-ABI of libmpc_ingest.so: native host ingest (Steps 1-3 of
- * /root/reference/src/mapped_paf_read_parser.py) for the drop-in CLI.
+ * mpc_ingest.h -- C-ABI of libmpc_ingest.so: the native host I/O of the drop-in
+ * CLI -- ingest (Steps 1-3 of /root/reference/src/mapped_paf_read_parser.py)
+ * and the Step 7 writers.
  *
  *   reference                                     replaced by
  *   --------------------------------------------  ----------------------------------
  *   Step 1 reference FASTA          :161-184      mpc_ingest(): ref
  *   Step 2 PAF, first alignment per read :192-245 mpc_ingest(): cs, tstart, qs/qe flip
  *   Step 3 reads FASTA, revcomp, flanks :253-277  mpc_ingest(): up, down
+ *   Step 7 writers                  :446-463      mpc_write_calls()
  *
  * Same results as minion-plasmid-consensus_amd/ingest.py (the Python
  * restatement of those steps): memory-mapped files, multi-threaded line
@@ -52,6 +54,17 @@ typedef struct {
 } mpc_ingest_out;
 
 int mpc_ingest_version(void);
+
+/* Step 7 writers (:446-463), native (csrc/writers.cpp).  calls = ONE sample's
+ * calls exactly as the device returns them (MPC_BUF_CALLS rows of include/mpc.h:
+ * uint32 x4 = {base | chrom1 << 8 | chrom2 << 16, count, count2, total}).
+ * Writes the consensus FASTA, the chromatogram TSV and the accuracies TSV in
+ * the reference's formats (accuracy = Python repr of 100 * (count / total) in
+ * f64); n_threads <= 0: all hardware threads.  0 on success, -1 with msg set. */
+int mpc_write_calls(const uint32_t* calls, int64_t n_calls, const char* consensus_path, const char* chromat_path,
+                    const char* accuracies_path, int n_threads, char* msg, int msg_len);
+/* Python's repr() of a float into out (NUL-terminated): its length, or -1 if out_len is too small. */
+int mpc_py_float_repr(double x, char* out, int out_len);
 /* n_threads <= 0: all hardware threads.  Returns out->status. */
 int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_path, int n_threads,
                mpc_ingest_out* out);

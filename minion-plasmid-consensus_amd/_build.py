@@ -3,7 +3,7 @@ the repo snapshot to the GPU box).
 
   libmpc.so        HIP kernels + C-ABI (include/mpc.h), hipcc --offload-arch=gfx950
   libmpc_synth.so  host-only synthetic data generator (g++)
-  libmpc_ingest.so native host ingest, Steps 1-3 (include/mpc_ingest.h, g++ -pthread)
+  libmpc_ingest.so native host I/O: ingest (Steps 1-3) and writers (Step 7) (include/mpc_ingest.h, g++ -pthread)
 """
 import os
 import subprocess
@@ -39,10 +39,10 @@ def ensure_synth():
 
 
 def build_ingest(force=False):
-    src = os.path.join(CSRC, "ingest.cpp")
+    srcs = [os.path.join(CSRC, "ingest.cpp"), os.path.join(CSRC, "writers.cpp")]
     hdr = os.path.join(INCLUDE, "mpc_ingest.h")
-    if force or _stale(LIBINGEST, [src, hdr]):
-        subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-I", INCLUDE, "-o", LIBINGEST, src],
+    if force or _stale(LIBINGEST, srcs + [hdr]):
+        subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-I", INCLUDE, "-o", LIBINGEST] + srcs,
                        check=True)
     return LIBINGEST
 

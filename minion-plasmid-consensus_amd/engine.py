@@ -338,6 +338,7 @@ class Plan:
         for s in range(self.batch.n_samples):
             c = calls[nc[s]: nc[s + 1]]
             out.append(dict(
+                raw=np.ascontiguousarray(c),  # the device rows (include/mpc.h MPC_BUF_CALLS), for the native writers
                 base=(c[:, 0] & 0xFF).astype(np.uint8), chrom1=((c[:, 0] >> 8) & 0xFF).astype(np.uint8),
                 chrom2=((c[:, 0] >> 16) & 0xFF).astype(np.uint8), count=c[:, 1].astype(np.int64),
                 count2=c[:, 2].astype(np.int64), total=c[:, 3].astype(np.int64), max_depth=int(md[s]),

@@ -160,6 +160,11 @@ def _native():
         L.mpc_ingest.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                  ctypes.POINTER(_IngestOut)]
         L.mpc_ingest_free.argtypes = [ctypes.POINTER(_IngestOut)]
+        L.mpc_write_calls.restype = ctypes.c_int
+        L.mpc_write_calls.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_char_p,
+                                      ctypes.c_char_p, ctypes.c_int, ctypes.c_char_p, ctypes.c_int]
+        L.mpc_py_float_repr.restype = ctypes.c_int
+        L.mpc_py_float_repr.argtypes = [ctypes.c_double, ctypes.c_char_p, ctypes.c_int]
         _ingest_lib = L
     return _ingest_lib or None
 

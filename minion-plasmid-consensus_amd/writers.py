@@ -4,7 +4,13 @@ consensus  ">consensus\\n" + called bases + "\\n"
 chromat    "pos\\tbase\\tcount" header, two lines per call (top, second) using the
            pre-GTF bases; pos is the 1-based index in the consensus
 accuracies "pos\\taccuracy" header, str(100 * (count / total)) per call
+
+The CLI writes through the native writer (csrc/writers.cpp, libmpc_ingest.so:
+all cores, Python float repr restated); the text functions below are the same
+formats in Python (tests compare the two).
 """
+import os
+
 import numpy as np
 
 
@@ -35,13 +41,44 @@ def accuracies_text(calls):
     return "".join(out)
 
 
-def write_outputs(calls, consensus_path, chromat_path, accuracies_path):
+class WriteError(OSError):
+    pass
+
+
+def write_outputs(calls, consensus_path, chromat_path, accuracies_path, n_threads=0):
+    """The three output files of one sample, from its device calls (``calls["raw"]``,
+    engine.Plan.fetch) through the native writer."""
+    import ctypes
+    from . import ingest
+    L = ingest._native()
+    if L is None:
+        raise WriteError("libmpc_ingest.so (native writers) is not built")
+    raw = np.ascontiguousarray(calls["raw"], dtype=np.uint32).reshape(-1, 4)
+    msg = ctypes.create_string_buffer(256)
+    buf = raw if raw.size else np.zeros((1, 4), np.uint32)
+    rc = L.mpc_write_calls(buf.ctypes.data, len(raw), os.fsencode(consensus_path), os.fsencode(chromat_path),
+                           os.fsencode(accuracies_path), int(n_threads), msg, 256)
+    if rc != 0:
+        raise WriteError(msg.value.decode(errors="replace"))
+
+
+def write_outputs_python(calls, consensus_path, chromat_path, accuracies_path):
+    """The same files through the Python text functions (tests, call dicts without ``raw``)."""
     with open(consensus_path, "w") as f:
         f.write(consensus_text(calls))
     with open(chromat_path, "w") as f:
         f.write(chromat_text(calls))
     with open(accuracies_path, "w") as f:
         f.write(accuracies_text(calls))
+
+
+def py_float_repr(x):
+    """repr(x) as the native writer prints it (tests)."""
+    import ctypes
+    from . import ingest
+    out = ctypes.create_string_buffer(40)
+    n = ingest._native().mpc_py_float_repr(float(x), out, 40)
+    return out.value[:n].decode()
 
 
 # Snakefile:77 (the rule's own table; no lower case, no 'X')

@@ -9,6 +9,7 @@
  *   Step 2 PAF, first alignment per read :192-245 mpc_ingest(): cs, tstart, qs/qe flip
  *   Step 3 reads FASTA, revcomp, flanks :253-277  mpc_ingest(): up, down
  *   Step 7 writers                  :446-463      mpc_write_calls()
+ *   src/pseudopair_reads.py         :92-140       mpc_pseudopair()
  *
  * Same results as minion-plasmid-consensus_amd/ingest.py (the Python
  * restatement of those steps): memory-mapped files, multi-threaded line
@@ -65,6 +66,21 @@ int mpc_write_calls(const uint32_t* calls, int64_t n_calls, const char* consensu
                     const char* accuracies_path, int n_threads, char* msg, int msg_len);
 /* Python's repr() of a float into out (NUL-terminated): its length, or -1 if out_len is too small. */
 int mpc_py_float_repr(double x, char* out, int out_len);
+
+/* src/pseudopair_reads.py:92-140 (rule pseudopair_reads, Snakefile:211-228), native
+ * (csrc/pseudopair.cpp): reads the PAF, writes the "fwd rev" pairs to out_path.
+ * has_min = 0: --min_align_length not given (TypeError in the script once reads
+ * remain).  Returns stats->status (MPC_INGEST_*; FALLBACK: use the Python
+ * restatement, minion-plasmid-consensus_amd/pseudopair_reads.py). */
+typedef struct {
+  int64_t n_fwd, n_rev;            /* tables after the PAF pass (:117) */
+  int64_t n_fwd_kept, n_rev_kept;  /* after the length filter (:135) */
+  int64_t n_pairs;
+  int32_t status;
+  char message[256];
+} mpc_pseudopair_stats;
+int mpc_pseudopair(const char* paf_path, int64_t min_align_length, int has_min, const char* out_path, int n_threads,
+                   mpc_pseudopair_stats* stats);
 /* n_threads <= 0: all hardware threads.  Returns out->status. */
 int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_path, int n_threads,
                mpc_ingest_out* out);

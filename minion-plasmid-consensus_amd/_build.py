@@ -39,7 +39,7 @@ def ensure_synth():
 
 
 def build_ingest(force=False):
-    srcs = [os.path.join(CSRC, "ingest.cpp"), os.path.join(CSRC, "writers.cpp")]
+    srcs = [os.path.join(CSRC, f) for f in ("ingest.cpp", "writers.cpp", "pseudopair.cpp")]
     hdr = os.path.join(INCLUDE, "mpc_ingest.h")
     if force or _stale(LIBINGEST, srcs + [hdr]):
         subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-I", INCLUDE, "-o", LIBINGEST] + srcs,

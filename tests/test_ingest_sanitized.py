@@ -1,4 +1,5 @@
-"""ASan + UBSan build of the native host ingest (csrc/ingest.cpp):
+"""ASan + UBSan build of the native host I/O (csrc/ingest.cpp, writers.cpp,
+pseudopair.cpp):
 a driver executable (tests/native/ingest_driver.cpp) built with
 -fsanitize=address,undefined and no recovery runs over every golden input, the
 edge / error / declined cases of test_ingest_native.py and synthetic files
@@ -34,8 +35,8 @@ def asan_bin():
     if shutil.which("g++") is None:
         pytest.skip("no g++")
     os.makedirs(os.path.dirname(BIN), exist_ok=True)
-    src = [os.path.join(REPO, "minion-plasmid-consensus_amd", "csrc", "ingest.cpp"),
-           os.path.join(REPO, "tests", "native", "ingest_driver.cpp")]
+    src = [os.path.join(REPO, "minion-plasmid-consensus_amd", "csrc", f) for f in
+           ("ingest.cpp", "writers.cpp", "pseudopair.cpp")] + [os.path.join(REPO, "tests", "native", "ingest_driver.cpp")]
     subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
                     "-fno-sanitize-recover=all", "-pthread", "-I", os.path.join(REPO, "include"), "-o", BIN] + src,
                    check=True)
@@ -98,3 +99,39 @@ def test_synthetic_sanitized(asan_bin, ing, tmp_path):
     syn.write_files(p["ref.fa"], p["reads.fa"], p["s.paf"], p["ras.fa"], p["as.paf"])
     _run(asan_bin, ing, p["ref.fa"], p["s.paf"], p["reads.fa"], threads=(1, 3, 8))
     _run(asan_bin, ing, p["ras.fa"], p["as.paf"], p["reads.fa"])
+
+
+def _san_env():
+    return dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:exitcode=86",
+                UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1:exitcode=87")
+
+
+def test_writers_sanitized(asan_bin, tmp_path):
+    w = importlib.import_module("minion-plasmid-consensus_amd.writers")
+    for n in (0, 1, 5000, 40000):
+        outs = [str(tmp_path / ("%s%d" % (x, n))) for x in ("c", "ch", "acc")]
+        p = subprocess.run([asan_bin, "writecalls", str(n), "7", *outs], capture_output=True, text=True,
+                           env=_san_env(), timeout=120)
+        assert p.returncode == 0 and p.stdout.strip() == "0", (n, p.stderr[-2000:])
+        assert open(outs[0]).read().startswith(">consensus\n")
+        assert open(outs[1]).read().count("\n") == 1 + 2 * n
+    assert w is not None
+
+
+def test_pseudopair_sanitized(asan_bin, tmp_path):
+    import test_pseudopair as tp
+    pp = importlib.import_module("minion-plasmid-consensus_amd.pseudopair_reads")
+    for case in tp.cases():
+        paf = tmp_path / (case + ".paf")
+        paf.write_bytes(tp.read(case, "in.paf"))
+        out = tmp_path / (case + ".out")
+        p = subprocess.run([asan_bin, "pseudopair", str(paf), "0", str(out)], capture_output=True, text=True,
+                           env=_san_env(), timeout=120)
+        assert p.returncode == 0, (case, p.stderr[-2000:])
+        status = int(p.stdout.split()[0])
+        try:
+            st = pp.pseudopair_native(str(paf), 0, str(tmp_path / "ref.out"))
+            exp = 2 if st is None else 0
+        except pp.PairError:
+            exp = 1
+        assert status == exp, case

@@ -187,7 +187,16 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
   int32_t* i_end; uint64_t* ins_raw; uint64_t* ins_sorted; int32_t* bk_cnt; int32_t* bk_off; int64_t* rbase;
   Ovf* ovf; uint32_t* ovf_cnt; uint32_t* hasleft; uint32_t* status;
   int32_t* diff; uint32_t* sub;
+  // tally mode 3: substitutions as 2-byte events per (wave, position window),
+  // tallied by K_subs (0 windows: global atomics)
+  uint16_t* subev; uint32_t* subev_cnt; int64_t subev_cap; int32_t sub_wins;
 };
+
+// Substitution events (tally mode 3, references too long for LDS substitution
+// tallies): position within a kSubWin-position window << 2 | code, per wave and
+// window in the wave's region [(cs_off[ra] - cs_base) / 3 + 2 ra, ...) of window
+// w's slice (a '*' token takes 3 cs bytes); K_subs tallies them per window in LDS.
+constexpr int kSubWinBits = 13, kSubWin = 1 << kSubWinBits, kMaxSubWins = 8;
 
 __host__ __device__ inline int parse_hl_words(int n) { return (n + 1 + 31) / 32; }
 __host__ __device__ constexpr int parse_misc_bytes() { return kMaxPW * 4 + kMaxPW * 8; }
@@ -586,6 +595,8 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int64_t wend = a.cs_off[rb];
   int64_t P = a.cs_off[ra];
   const int64_t ev_base = (P - a.cs_base) / 2 + 3 * ra;  // this wave's event region in ins_raw
+  const int64_t sev_base = (P - a.cs_base) / 3 + 2 * ra;  // ... and its substitution-event regions (TM 3)
+  uint32_t nsub_v = 0;                                    // lane k: substitution events of window k
   uint32_t nev = 0;                                       // events written (wave-uniform)
   int64_t rs0 = ra;         // first read whose cs starts at or after P
   bool carry = false;       // slot 0 holds a read continuing into this window
@@ -850,7 +861,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if (kind == 3 && (uint32_t)i > (uint32_t)n) te |= DE_INDEX;
       const int rl = q_read;
       if (te == 0) {
-        if (kind == 2) odd_sub(i, (int)pay);
+        if (kind == 2 && (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
         if (kind == 4 && i >= 0 && i < n) {
           depth_dec(i);
           depth_inc(i + olen_e < n ? i + olen_e : n);
@@ -858,6 +869,19 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         if (kind == 3) {
           atomicOr(hl + (i >> 5), 1u << (i & 31));
           if (olen_e > kInsInline) push_ovf(a, A + sx + 1, rl, i, olen_e);
+        }
+      }
+      if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window
+        const bool sev = te == 0 && kind == 2;
+        const int win = i >> kSubWinBits;
+        for (int ww = 0; ww < a.sub_wins; ++ww) {
+          const uint64_t bw = ballot(sev && win == ww);
+          if (!bw) continue;
+          const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)nsub_v, ww);
+          if (sev && win == ww)
+            a.subev[(int64_t)ww * a.subev_cap + sev_base + n0 + lanes_below(bw)] =
+                (uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay);
+          if (l == ww) nsub_v += (uint32_t)__popcll(bw);
         }
       }
       const bool ins_inline = kind == 3 && olen_e <= kInsInline && te == 0;
@@ -906,11 +930,62 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     a.i_end[r] = ts < 0 ? 0 : (ts > n ? n + 1 : ts);
   }
   if (l == 0) { wcnt[w] = nev; wbase[w] = ev_base; }
+  if (TM == 3 && l < a.sub_wins) a.subev_cnt[((int64_t)blockIdx.x * kMaxPW + w) * kMaxSubWins + l] = nsub_v;
   __syncthreads();
   parse_epilogue<TM>(a, n, gb, nbk, r0, hl, bcnt, uni, wcnt, wbase, nw, reinterpret_cast<uint64_t*>(lds),
                      nw * (int)sizeof(WL) / 8);
 }
 
+
+// ---------------------------------------------------------------------------
+// K_subs (tally mode 3): the substitution events of a sample's parse waves for
+// one kSubWin-position window, tallied in LDS (the event word IS the counter
+// index: position << 2 | code) and flushed with contiguous atomics.  One block
+// per (sample, window, chunk of <= kSubsWG parse workgroups); wave v walks the
+// chunk's regions v, v + 16, ... (8 loads in flight per lane).
+// ---------------------------------------------------------------------------
+constexpr int kSubsWG = 4;
+struct SubsArgs {
+  const int4* work;    // {sample, window, first parse workgroup, end}
+  const int4* pwork;   // parse work table {sample, r0, r1, 0}
+  const int64_t* cs_off; int64_t cs_base;
+  const uint16_t* subev; const uint32_t* subev_cnt; int64_t subev_cap;
+  const int32_t* n_of; const int32_t* gbase; uint32_t* sub;
+  int32_t nw_parse;
+};
+__global__ __launch_bounds__(1024) void K_subs(SubsArgs a) {
+  __shared__ uint32_t cnt[kSubWin * 4];
+  const int4 wk = a.work[blockIdx.x];
+  const int smp = wk.x, win = wk.y, pw0 = wk.z, pw1 = wk.w;
+  const int nreg = (pw1 - pw0) * a.nw_parse, l = lane(), v = threadIdx.x >> 6, nv = blockDim.x >> 6;
+  for (int k = threadIdx.x; k < kSubWin * 4; k += blockDim.x) cnt[k] = 0;
+  __syncthreads();
+  for (int rg = v; rg < nreg; rg += nv) {
+    const int pw = pw0 + rg / a.nw_parse, ww = rg % a.nw_parse;
+    const int4 pk = a.pwork[pw];
+    const int64_t ra = pk.y + (int64_t)(pk.z - pk.y) * ww / a.nw_parse;
+    const int c = (int)a.subev_cnt[((int64_t)pw * kMaxPW + ww) * kMaxSubWins + win];
+    const uint16_t* src = a.subev + (int64_t)win * a.subev_cap + (a.cs_off[ra] - a.cs_base) / 3 + 2 * ra;
+    for (int e0 = 0; e0 < c; e0 += 8 * 64) {
+      uint32_t ev[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int e = e0 + l + 64 * u;
+        ev[u] = e < c ? (uint32_t)src[e] : ~0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u)
+        if (ev[u] != ~0u) atomicAdd(&cnt[ev[u]], 1u);
+    }
+  }
+  __syncthreads();
+  const int64_t p0 = (int64_t)win * kSubWin, n = a.n_of[smp];
+  uint32_t* dst = a.sub + ((int64_t)a.gbase[smp] + p0) * 4;
+  for (int k = threadIdx.x; k < kSubWin * 4; k += blockDim.x) {  // consecutive lanes, consecutive words
+    const uint32_t x = cnt[k];
+    if (x && p0 + (k >> 2) < n) atomicAdd(dst + k, x);
+  }
+}
 
 // ---------------------------------------------------------------------------
 // Downstream (RIGHT) events.  A gap holding only RIGHT events needs only its
@@ -2092,7 +2167,9 @@ struct mpc_plan {
   int end_bit = 0;
   size_t ws_bytes = 0;
   uint8_t* ws = nullptr;
-  std::vector<int32_t> work_parse, work_bc;  // int4 records
+  std::vector<int32_t> work_parse, work_bc, work_sub;  // int4 records
+  int32_t sub_wins = 0;                               // tally mode 3: substitution-event windows
+  int64_t subev_cap = 0;
   int n_parse_wg = 0, parse_lds = 0, nbmax = 1, parse_win = 1024, parse_nw = 8;
   int64_t n_bc = 0, units_cap = 0, max_wg_reads = 0;
   int32_t shard = 0, n_shards = 1;
@@ -2102,7 +2179,8 @@ struct mpc_plan {
     B_HASLEFT, B_KIN, B_VIN, B_KOUT, B_VOUT, B_KTMP, B_VTMP, B_BCNT, B_BPRE, B_RLEN, B_RPOS, B_RSTART, B_RSLOC, B_ROFF, B_RCNT, B_RCNTALL,
     // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
     B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
-    B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_RUNT, B_COUNT
+    B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_RUNT,
+    B_SUBEV, B_SUBCNT, B_WSUB, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -2157,6 +2235,8 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.hasleft = d.hasleft; a.status = d.status;
   a.diff = d.diff; a.sub = d.sub;
+  a.subev = at<uint16_t>(p, mpc_plan::B_SUBEV); a.subev_cnt = at<uint32_t>(p, mpc_plan::B_SUBCNT);
+  a.subev_cap = p->subev_cap; a.sub_wins = p->tally_mode == 3 ? p->sub_wins : 0;
   return a;
 }
 
@@ -2167,6 +2247,15 @@ static const void* parse_kernel(int tm, int win) {
   if (win == 512) return tm ? (const void*)K_parse<1, 512> : (const void*)K_parse<0, 512>;
   if (win == 2048) return tm ? (const void*)K_parse<1, 2048> : (const void*)K_parse<0, 2048>;
   return tm ? (const void*)K_parse<1, 1024> : (const void*)K_parse<0, 1024>;
+}
+static void launch_subs(const mpc_plan* p, const Dev& d, hipStream_t st) {
+  if (p->work_sub.empty()) return;
+  SubsArgs a;
+  a.work = at<const int4>(p, mpc_plan::B_WSUB); a.pwork = at<const int4>(p, mpc_plan::B_WPARSE);
+  a.cs_off = d.cs_off; a.cs_base = d.cs_base;
+  a.subev = at<uint16_t>(p, mpc_plan::B_SUBEV); a.subev_cnt = at<uint32_t>(p, mpc_plan::B_SUBCNT);
+  a.subev_cap = p->subev_cap; a.n_of = d.n_of; a.gbase = d.gbase; a.sub = d.sub; a.nw_parse = p->parse_nw;
+  hipLaunchKernelGGL(K_subs, dim3((unsigned)(p->work_sub.size() / 4)), dim3(1024), 0, st, a);
 }
 static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
   const dim3 g(p->n_parse_wg), b(p->parse_nw * 64);
@@ -2334,15 +2423,30 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       }
     if (best < 0) { delete p; return fail(MPC_E_ARG, "reference too long for the LDS budget"); }
     p->parse_lds = lds_of(p->parse_win, p->tally_mode, p->parse_nw);
+    // workgroups per sample: the smallest largest-chunk R with sum_s ceil(ns / R)
+    // <= the resident slots (256 CUs x per_cu), so that the parse is one balanced
+    // wave of workgroups (C5: 24 samples x 10 instead of x 11 = 264 > 256 slots,
+    // whose 8 second-wave workgroups doubled K_parse); >= 64 reads per workgroup
     const int64_t target = 256 * per_cu;
+    const int64_t wcap = wg_reads_cap(p->tally_mode);
+    auto chunks = [&](int64_t ns, int64_t R) {
+      int64_t ch = (ns + R - 1) / R;
+      ch = std::min<int64_t>(ch, (ns + 63) / 64);
+      return std::max<int64_t>(ch, (ns + wcap - 1) / wcap);
+    };
+    int64_t R_lo = 1, R_hi = std::max<int64_t>(p->N, 1);
+    while (R_lo < R_hi) {
+      const int64_t mid = (R_lo + R_hi) / 2;
+      int64_t tot = 0;
+      for (int s = 0; s < p->S; ++s) tot += chunks(p->read_begin[s + 1] - p->read_begin[s], mid);
+      if (tot <= target) R_hi = mid; else R_lo = mid + 1;
+    }
     std::vector<int> pw_begin(p->S + 1, 0);
     for (int s = 0; s < p->S; ++s) {
       pw_begin[s] = (int)(p->work_parse.size() / 4);
       const int64_t a = p->read_begin[s], b = p->read_begin[s + 1], ns = b - a;
       if (ns <= 0) continue;
-      int64_t ch = std::max<int64_t>(1, (target * ns + std::max<int64_t>(p->N, 1) - 1) / std::max<int64_t>(p->N, 1));
-      ch = std::min<int64_t>(ch, (ns + 63) / 64);
-      ch = std::max<int64_t>(ch, (ns + wg_reads_cap(p->tally_mode) - 1) / wg_reads_cap(p->tally_mode));
+      const int64_t ch = chunks(ns, R_lo);
       for (int64_t c = 0; c < ch; ++c) {
         const int64_t x = a + ns * c / ch, y = a + ns * (c + 1) / ch;
         if (y > x) p->work_parse.insert(p->work_parse.end(), {s, (int32_t)x, (int32_t)y, 0});
@@ -2351,6 +2455,15 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     }
     pw_begin[p->S] = (int)(p->work_parse.size() / 4);
     p->n_parse_wg = pw_begin[p->S];
+    // tally mode 3: substitutions as events per kSubWin-position window (K_subs)
+    p->sub_wins = 0;
+    if (p->tally_mode == 3 && n_max <= (int64_t)kSubWin * kMaxSubWins) {
+      p->sub_wins = (int32_t)((n_max + kSubWin - 1) / kSubWin);
+      for (int s = 0; s < p->S; ++s)
+        for (int w = 0; w * (int64_t)kSubWin < p->ref_len[s]; ++w)
+          for (int c = pw_begin[s]; c < pw_begin[s + 1]; c += kSubsWG)
+            p->work_sub.insert(p->work_sub.end(), {s, w, c, std::min(c + kSubsWG, pw_begin[s + 1])});
+    }
     for (int s = 0; s < p->S; ++s) {
       const int nb = (int)((p->ref_len[s] + 1 + kBW - 1) / kBW);
       if (pw_begin[s + 1] == pw_begin[s]) continue;  // no reads: nothing to tally
@@ -2415,6 +2528,10 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_WBC, (int64_t)p->work_bc.size(), 4);
   set(mpc_plan::B_UNITS, p->units_cap * 8, 4);  // 2 int4 per unit
   set(mpc_plan::B_RUNT, RU * 16, 4);            // per run: inline LEFT bases [bi from the 3' end][code]
+  p->subev_cap = p->sub_wins ? in->cs_bytes / 3 + 2 * N + 16 : 0;
+  set(mpc_plan::B_SUBEV, p->subev_cap * p->sub_wins, 2);
+  set(mpc_plan::B_SUBCNT, p->sub_wins ? (int64_t)p->n_parse_wg * kMaxPW * kMaxSubWins : 0, 4);
+  set(mpc_plan::B_WSUB, (int64_t)p->work_sub.size(), 4);
   size_t o = 0;
   for (int b = 0; b < mpc_plan::B_COUNT; ++b) {
     o = (o + 255) & ~(size_t)255;
@@ -2470,6 +2587,8 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WPARSE), p->work_parse.data(), 4 * p->work_parse.size(), hipMemcpyHostToDevice));
   if (!p->work_bc.empty())
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WBC), p->work_bc.data(), 4 * p->work_bc.size(), hipMemcpyHostToDevice));
+  if (!p->work_sub.empty())
+    HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WSUB), p->work_sub.data(), 4 * p->work_sub.size(), hipMemcpyHostToDevice));
   HIPCHK(hipFuncSetAttribute(parse_kernel(p->tally_mode, p->parse_win), hipFuncAttributeMaxDynamicSharedMemorySize,
                              p->parse_lds));
   p->bound = true;
@@ -2532,8 +2651,10 @@ int mpc_parse(mpc_plan* p, void* stream) {
     HIPCHK(hipGetLastError());
     p->runt_dirty = false;  // only once the clear is enqueued
   }
-  if (p->n_parse_wg > 0)
+  if (p->n_parse_wg > 0) {
     launch_parse(p, d, st);
+    launch_subs(p, d, st);
+  }
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """Time the parse phase ALONE (K_clear + K_parse, HIP events) of library
 variants; later phases never run, so experiment builds that skip stores are
-safe.   KEXP_CFG=c2|c4 python3 scripts/kparse_only.py lib1.so [lib2.so ...]"""
+safe.   KEXP_CFG=c1..c5 (bench.py workloads) python3 scripts/kparse_only.py lib1.so [lib2.so ...]"""
 import os, subprocess, sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -13,10 +13,9 @@ pkg = importlib.import_module("minion-plasmid-consensus_amd")
 eng = pkg.engine
 eng.set_library(os.environ["KEXP_LIB"])  # variant build under test (experiments only)
 cfg = os.environ.get("KEXP_CFG", "c2")
-n, reads, prof, seed, anti = {"c2": (2686, 100000, "default", 2, True), "c4": (10000, 100000, "indel", 4, True), "c5": (30000, 10000, "default", 5000, True),
-                              "c3": (10000, 125000, "default", 3, False)}[cfg]
-syn = pkg.synth.Synth(n=n, n_reads=reads, profile=prof, seed=seed, antisense=anti)
-samples = [syn.sample(s) for s in range(2 if anti else 1)]
+sys.path.insert(0, %r)
+import bench
+samples, _ = bench.shard_samples(pkg, cfg, 0, 1)
 plan = eng.Plan(eng.Batch(samples))
 st = torch.cuda.current_stream()
 for _ in range(3): plan.phase("parse")
@@ -26,7 +25,7 @@ for a, b in ev:
     a.record(st); plan.phase("parse"); b.record(st)
 torch.cuda.synchronize()
 print("KP %%.1f" %% float(np.median([a.elapsed_time(b) for a, b in ev]) * 1e3), [int(x) for x in plan.status()][:4])
-''' % REPO
+''' % (REPO, REPO)
 for lib in sys.argv[1:]:
     env = dict(os.environ, KEXP_LIB=os.path.abspath(lib))
     p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)

@@ -944,7 +944,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
 // per (sample, window, chunk of <= kSubsWG parse workgroups); wave v walks the
 // chunk's regions v, v + 16, ... (8 loads in flight per lane).
 // ---------------------------------------------------------------------------
-constexpr int kSubsWG = 4;
+constexpr int kSubsWG = 32;  // parse workgroups per K_subs block, at most
 struct SubsArgs {
   const int4* work;    // {sample, window, first parse workgroup, end}
   const int4* pwork;   // parse work table {sample, r0, r1, 0}
@@ -1347,11 +1347,11 @@ __global__ __launch_bounds__(kRS) void K_rsplit_units(Dev d, UnitArgs ua, int32_
 
 // A unit record (2 int4, written by units_block): {sample, bucket, pw0, pw1},
 // {e0, cnt, n, gbase}.  Per unit: the entry's <= 256 slices (counts, sources)
-// lane-parallel, block scan; afterwards event e of the entry is
+// lane-parallel, block scan (s_pre[256]: the entry's total); afterwards event e of the entry is
 // ins_sorted[s_src[j] + e - s_pre[j]] with j = the last slice whose s_pre <= e.
 // The per-gap tables of the bucket (global run range, this shard's sorted-RIGHT
 // range; K_ins: the anchor row) are loaded in the same round trip.
-struct UnitView { int smp, bucket, e0, cnt, n, gb, g0, gl; int64_t R0, R1; };
+struct UnitView { int smp, bucket, e0, cnt, n, gb, g0, gl, nsl; int64_t R0, R1; };
 template <bool ANC>
 __device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, const int32_t* bk_cnt,
                                               const int32_t* bk_off, const int64_t* rbase, int nbs,
@@ -1361,7 +1361,7 @@ __device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, cons
                                               int32_t* s_rs, int32_t* s_rsl, int32_t* s_roff, int32_t* s_anc) {
   const int4 ua = units[2 * u], ub = units[2 * u + 1];
   UnitView v;
-  v.smp = ua.x; v.bucket = ua.y; v.e0 = ub.x; v.cnt = ub.y; v.n = ub.z; v.gb = ub.w;
+  v.smp = ua.x; v.bucket = ua.y; v.e0 = ub.x; v.cnt = ub.y; v.n = ub.z; v.gb = ub.w; v.nsl = ua.w - ua.z;
   v.g0 = v.bucket * kBW;
   v.gl = v.g0 + kBW - 1 < v.n ? v.g0 + kBW - 1 : v.n;  // last gap of the bucket
   const int l = lane(), w = threadIdx.x >> 6;
@@ -1401,17 +1401,28 @@ __device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, cons
     int wpre = 0;
     for (int k = 0; k < w; ++k) wpre += s_wsum[k];
     s_pre[tid] += wpre;
+    if (tid == 255) s_pre[256] = s_pre[tid] + cnt;  // the entry's events
   }
   __syncthreads();
   return v;
 }
-__device__ __forceinline__ int64_t unit_event_src(const int32_t* s_pre, const int64_t* s_src, int e) {
-  int lo = 0, hi = 255;  // last slice j with s_pre[j] <= e
+// the last slice j >= j0 with s_pre[j] <= e (j0 < 0: no hint): up to 3 linear
+// steps from the hint, else a binary search of the rest
+__device__ __forceinline__ int unit_slice_next(const int32_t* s_pre, int e, int j0) {
+  int lo = j0 < 0 ? 0 : j0;
+  if (j0 >= 0) {
+#pragma unroll
+    for (int t = 0; t < 3; ++t) {
+      if (lo == 255 || s_pre[lo + 1] > e) return lo;
+      ++lo;
+    }
+  }
+  int hi = 255;
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
     if (s_pre[mid] <= e) lo = mid; else hi = mid - 1;
   }
-  return s_src[lo] + (e - s_pre[lo]);
+  return lo;
 }
 
 
@@ -1443,7 +1454,7 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
   // different bank (unpadded, all gaps' run-0 counters shared 16 banks)
   constexpr int kMs = kKMax + 1, kTs = kKMax * 16 + 1;
   __shared__ uint32_t Ml[kBW * kMs];
-  __shared__ int32_t s_pre[256];
+  __shared__ int32_t s_pre[257];
   __shared__ int64_t s_src[256];
   __shared__ int32_t s_wsum[4];
   __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1];  // per gap of the bucket (K_left)
@@ -1460,10 +1471,20 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
     const int gb = uv.gb;
     const int g0 = uv.g0;
     uint64_t evs[kEPT];
+    // all loads first (latency), then the tallies.  The thread's events move
+    // kUB apart: with >= kUB events per slice on average (C3 / C4) its slice is
+    // searched once, then advanced; with short slices (C2) every event's search
+    // is independent (a chain of advancing searches would serialize them)
+    const bool adv = s_pre[256] >= kUB * uv.nsl;
+    int js = -1;
 #pragma unroll
-    for (int q = 0; q < kEPT; ++q) {  // all loads first (latency), then the tallies
+    for (int q = 0; q < kEPT; ++q) {
       const int e = uv.e0 + (int)threadIdx.x + q * kUB;
-      evs[q] = e < uv.e0 + uv.cnt ? a.ins_sorted[unit_event_src(s_pre, s_src, e)] : ~0ull;
+      evs[q] = ~0ull;
+      if (e < uv.e0 + uv.cnt) {
+        js = unit_slice_next(s_pre, e, adv ? js : -1);
+        evs[q] = a.ins_sorted[s_src[js] + (e - s_pre[js])];
+      }
     }
     // the run of an event at a mixed gap is a search of the gap's RIGHT reads:
     // stage the bucket's (contiguous in vals_out) in LDS, so no event waits on
@@ -2406,15 +2427,20 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
                            : parse_lds_bytes<1024>((int)n_max, tm, p->nbmax, nw);
     };
     // score = resident waves x window efficiency (measured at C2: 512 B windows
-    // cost ~25 % more per byte than 2 KiB ones, 1 KiB ~5 %).  Global substitution
-    // atomics (tm 3) lost to tm 2 with fewer waves at C3 (711 vs 491 us) though
-    // they won at C4 (3769 vs 4614 us): tm 3 only when tm 1 / 2 do not fit.
-    static const int cand[10][2] = {{1, 2048}, {2, 2048}, {1, 1024}, {2, 1024}, {1, 512},
-                                    {3, 2048}, {3, 1024}, {0, 2048}, {0, 1024}, {0, 512}};
+    // cost ~25 % more per byte than 2 KiB ones, 1 KiB ~5 %).  Tally mode 3 keeps
+    // only depth in LDS; its substitutions are window events (K_subs) while the
+    // reference fits kMaxSubWins windows, and then it competes on score: at C3 /
+    // C4 (10 kb) its 16 waves beat tm 2's 12 (parse 3060 -> 2947 us, 3396 ->
+    // 3004 us), at C2 tm 1 with 16 waves wins the tie (167 vs 197 us).  Beyond
+    // that its substitutions are global atomics: only when tm 1 / 2 do not fit.
+    const bool sub_events = n_max <= (int64_t)kSubWin * kMaxSubWins;
+    static const int cand[10][2] = {{1, 2048}, {2, 2048}, {1, 1024}, {2, 1024}, {3, 2048}, {3, 1024},
+                                    {1, 512}, {0, 2048}, {0, 1024}, {0, 512}};
     int best = -1, per_cu = 1;
-    for (const auto& c : cand)  // tm 3 only when neither 1 nor 2 fits, tm 0 only when no LDS mode fits
+    for (const auto& c : cand)
       for (int nw : {16, 12, 8}) {
-        if ((c[0] == 0 || c[0] == 3) && best > 0 && (c[0] == 0 || p->tally_mode != 3)) break;
+        if (c[0] == 3 && !sub_events && best > 0) break;  // global-atomic tm 3 only when nothing else fits
+        if (c[0] == 0 && best > 0) break;                  // tm 0 only when no LDS mode fits
         const int lds = lds_of(c[1], c[0], nw);
         if (lds > lds_cap) continue;
         const int wgs = std::max(1, std::min(lds_cap / lds, max_waves_cu / nw));
@@ -2457,12 +2483,18 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     p->n_parse_wg = pw_begin[p->S];
     // tally mode 3: substitutions as events per kSubWin-position window (K_subs)
     p->sub_wins = 0;
-    if (p->tally_mode == 3 && n_max <= (int64_t)kSubWin * kMaxSubWins) {
+    if (p->tally_mode == 3 && sub_events) {
       p->sub_wins = (int32_t)((n_max + kSubWin - 1) / kSubWin);
+      // parse workgroups per K_subs block: about one block per CU (each block's
+      // LDS tally is 128 KiB; more blocks = more flush atomics, fewer = fewer CUs)
+      int64_t pairs = 0;
+      for (int s = 0; s < p->S; ++s)
+        pairs += ((p->ref_len[s] + kSubWin - 1) / kSubWin) * (int64_t)(pw_begin[s + 1] - pw_begin[s]);
+      const int kc = (int)std::min<int64_t>(kSubsWG, std::max<int64_t>(1, (pairs + 255) / 256));
       for (int s = 0; s < p->S; ++s)
         for (int w = 0; w * (int64_t)kSubWin < p->ref_len[s]; ++w)
-          for (int c = pw_begin[s]; c < pw_begin[s + 1]; c += kSubsWG)
-            p->work_sub.insert(p->work_sub.end(), {s, w, c, std::min(c + kSubsWG, pw_begin[s + 1])});
+          for (int c = pw_begin[s]; c < pw_begin[s + 1]; c += kc)
+            p->work_sub.insert(p->work_sub.end(), {s, w, c, std::min(c + kc, pw_begin[s + 1])});
     }
     for (int s = 0; s < p->S; ++s) {
       const int nb = (int)((p->ref_len[s] + 1 + kBW - 1) / kBW);

@@ -55,12 +55,14 @@ def test_planner_geometry(pkg):
     c2 = g([2686, 2686], [100_000, 100_000], 63 << 20)
     assert c2["tally_mode"] == 1 and c2["max_reads_per_workgroup"] <= c2["reads_per_workgroup_cap"] == 32767
     c3 = g([10_000], [1_000_000], 1200 << 20)
-    assert c3["tally_mode"] == 2 and c3["max_reads_per_workgroup"] <= c3["reads_per_workgroup_cap"] == 16383
+    assert c3["tally_mode"] == 3 and c3["max_reads_per_workgroup"] <= c3["reads_per_workgroup_cap"] == 16383
     c5 = g([30_000] * 24, [10_000] * 24, 24 * 3600 * 10_000 // 100)
-    assert c5["tally_mode"] in (2, 3)
+    assert c5["tally_mode"] == 3
+    m6 = g([6000, 6000], [100_000, 100_000], 150 << 20)  # 10-byte packed tallies between tm 1 and tm 3
+    assert m6["tally_mode"] == 2 and m6["parse_waves"] == 16
     # the cap binds: 4.9 M tiny reads beside one 10 kb sample put 16383 reads in a workgroup
     st = g([10_000, 30], [100, 16383 * 300], 16383 * 300 * 12)
-    assert st["tally_mode"] == 2
+    assert st["tally_mode"] == 3
     assert st["max_reads_per_workgroup"] == st["reads_per_workgroup_cap"] == 16383
-    for info in (c2, c3, c5, st):
+    for info in (c2, c3, c5, m6, st):
         assert info["parse_lds_bytes"] <= 160 * 1024 and info["parse_waves"] in (8, 12, 16)

@@ -8,8 +8,8 @@ against the oracle's full pileup filtered by the reference's two tests
 (depth_util.derive).  Matches mapped_paf_read_parser.py:292-439 at depth.
 
 Plus the 16-bit LDS tally bound of K_parse: batches whose parse workgroups
-hold exactly the reads-per-workgroup cap (mpc_plan_info), in both LDS tally
-modes.
+hold exactly the reads-per-workgroup cap (mpc_plan_info), in every LDS tally
+mode (tm 1 12-byte, tm 2 10-byte packed, tm 3 depth-only + substitution events).
 """
 import importlib
 
@@ -21,7 +21,7 @@ import depth_util as du
 pytestmark = pytest.mark.gpu
 
 CONFIG_CASES = ["c1", "c2", "c3", "c4", "c5_slice", "c5"]
-EXPECT_MODE = {"c1": 1, "c2": 1, "c3": 2, "c4": 2, "c5_slice": 3, "c5": 3}
+EXPECT_MODE = {"c1": 1, "c2": 1, "c3": 3, "c4": 3, "c5_slice": 3, "c5": 3}
 
 
 def _samples(pkg, case):
@@ -60,24 +60,26 @@ def test_config_full_size(pkg, case):
     _check(pkg, samples, case, EXPECT_MODE[case])
 
 
-def _tiny_reads_batch(pkg, n_tiny, big_reads=100):
-    """One 10 kb sample with a few reads (sets the packed tally mode) and one
+def _tiny_reads_batch(pkg, n_tiny, big_n, big_reads=100):
+    """One ``big_n`` bp sample with a few reads (sets the tally mode) and one
     30 bp sample with ``n_tiny`` reads: its parse workgroups fill up to the
     reads-per-workgroup cap; high substitution / deletion rates and partial
     reads put many updates on every position's 16-bit counters."""
-    a = pkg.synth.Synth(n=10_000, n_reads=big_reads, profile="default", seed=61, antisense=False)
+    a = pkg.synth.Synth(n=big_n, n_reads=big_reads, profile="default", seed=61, antisense=False)
     b = pkg.synth.Synth(n=30, n_reads=n_tiny, profile="default", seed=62, antisense=False, frac_partial=0.5,
                         flank=(0, 6), p_sub=0.4, p_del=0.1, p_ins=0.1, del_len=(1, 2), ins_len=(1, 2))
     return [a.sample(0), b.sample(0)]
 
 
 @pytest.mark.timeout(600)
-def test_workgroup_cap_packed_tallies(pkg):
-    """Tally mode 2 (10-byte packed LDS tallies: C3 / C4): 16383 reads per workgroup."""
-    samples = _tiny_reads_batch(pkg, 16383 * 300)
+@pytest.mark.parametrize("big_n,mode", [(6_000, 2), (10_000, 3)])
+def test_workgroup_cap_packed_tallies(pkg, big_n, mode):
+    """Tally modes 2 (10-byte packed LDS tallies) and 3 (LDS depth, substitution
+    events: C3 / C4 / C5): 16383 reads per workgroup."""
+    samples = _tiny_reads_batch(pkg, 16383 * 300, big_n)
     info = pkg.engine.Plan(pkg.engine.Batch(samples)).info()
-    assert info["tally_mode"] == 2 and info["max_reads_per_workgroup"] == info["reads_per_workgroup_cap"] == 16383
-    _check(pkg, samples, "cap_tm2", 2)
+    assert info["tally_mode"] == mode and info["max_reads_per_workgroup"] == info["reads_per_workgroup_cap"] == 16383
+    _check(pkg, samples, "cap_tm%d" % mode, mode)
 
 
 @pytest.mark.timeout(600)

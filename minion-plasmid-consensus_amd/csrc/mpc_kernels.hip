@@ -49,6 +49,7 @@ constexpr int kICap = 1 << 28;      // saturation of the running coordinate i
 #define MPC_BW 64
 #endif
 constexpr int kBW = MPC_BW;         // gaps per insertion bucket (K_left workgroup)
+static_assert(kBW <= 64 && (kBW & (kBW - 1)) == 0, "sorted insertion events hold the gap within its bucket in 6 bits");
 constexpr int kKMax = 8;            // runs per gap tallied in K_left's LDS (others go to HBM)
 constexpr uint32_t kNullGap = 0x3fffffu;
 
@@ -65,14 +66,15 @@ struct Ovf {  // long insertion (len > kInsInline), tallied by K_flank
 __device__ __forceinline__ uint64_t ins_event(int gap, int len, uint32_t bases, int64_t rg) {
   return ((uint64_t)(uint32_t)rg << 32) | ((uint32_t)gap << 10) | ((uint32_t)(len - 1) << 8) | bases;
 }
-// flank event: bit 63 set, bit 62 = downstream (RIGHT) flank, bits 32..61 =
-// global read, gap << 10.  Bucket-sorted with the insertion events (separate
-// buckets) so K_left / K_flank find the flanks anchored at their gaps.
-constexpr uint64_t kFlankBit = 1ull << 63, kDownBit = 1ull << 62;
-__device__ __forceinline__ uint64_t flank_event(int gap, bool down, int64_t rg) {
-  return kFlankBit | (down ? kDownBit : 0ull) | ((uint64_t)((uint32_t)rg & 0x3fffffffu) << 32) | ((uint32_t)gap << 10);
+// bucket-sorted insertion event (ins_sorted, what K_left reads): 4 bytes, the
+// bucket and the parse workgroup are implied by the slice it lies in --
+// bases (8 bits) | (len-1) << 8 | gap within the kBW-gap bucket << 10 |
+// read relative to the workgroup's first read << 16 (< 2^15: wg_reads_cap);
+// bit 31 clear (~0u: no event)
+__device__ __forceinline__ uint32_t sorted_event(uint64_t raw, int64_t rg0) {
+  const uint32_t gap = (uint32_t)(raw >> 10) & 0x3fffffu;
+  return ((uint32_t)raw & 0x3ffu) | ((gap % (uint32_t)kBW) << 10) | ((uint32_t)((int64_t)(raw >> 32) - rg0) << 16);
 }
-__device__ __forceinline__ int64_t event_read(uint64_t ev) { return (int64_t)((ev >> 32) & 0x3fffffffu); }
 
 struct Dev {  // device-side views of the plan for the small kernels (passed by value)
   const uint8_t* ref; const int64_t* ref_off;
@@ -184,7 +186,7 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
   const int4* work;  // per workgroup: {sample, first read, end read, 0}
   int64_t cs_base, ovf_cap, read_offset, n_reads;
   int32_t nbs;       // bucket slots per parse workgroup (max buckets)
-  int32_t* i_end; uint64_t* ins_raw; uint64_t* ins_sorted; int32_t* bk_cnt; int32_t* bk_off; int64_t* rbase;
+  int32_t* i_end; uint64_t* ins_raw; uint32_t* ins_sorted; int32_t* bk_cnt; int32_t* bk_off; int64_t* rbase;
   Ovf* ovf; uint32_t* ovf_cnt; uint32_t* hasleft; uint32_t* status;
   int32_t* diff; uint32_t* sub;
   // tally mode 3: substitutions as 2-byte events per (wave, position window),
@@ -468,7 +470,8 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, int64
   // free now), then written out so that consecutive lanes store consecutive
   // addresses of a bucket's run (8-byte scattered stores left most 128-byte
   // lines partially written: ~8x HBM write amplification at C4)
-  uint64_t* dst = a.ins_sorted + rb_wg;
+  uint32_t* dst = a.ins_sorted + rb_wg;
+  const int64_t rg0 = a.read_offset + r0;  // the workgroup's first (global) read
   uint32_t* ccnt = bcur + nbk;  // [nbk] per-chunk bucket counts
   uint32_t* coff = ccnt + nbk;  // [nbk + 1] their exclusive scan (coff[nbk]: events staged)
   const int chunk = min(stg_cap, kEpiU * bstride);
@@ -516,7 +519,7 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, int64
     for (int j = threadIdx.x; j < staged; j += bstride) {
       const uint64_t e = stg[j];
       const int b = (int)(((uint32_t)(e >> 10) & kNullGap) / kBW);
-      dst[bcur[b] + (j - (int)coff[b])] = e;
+      dst[bcur[b] + (j - (int)coff[b])] = sorted_event(e, rg0);
     }
     __syncthreads();
     for (int k = threadIdx.x; k < nbk; k += bstride) { bcur[k] += ccnt[k]; ccnt[k] = 0; }
@@ -1357,6 +1360,7 @@ __device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, cons
                                               const int32_t* bk_off, const int64_t* rbase, int nbs,
                                               const int32_t* right_start, const int32_t* rsl, const int32_t* roff,
                                               const int32_t* row_base, const int32_t* lo_f, const int32_t* rowcnt,
+                                              const int4* pwork, int32_t* s_r0,
                                               int32_t* s_pre, int64_t* s_src, int32_t* s_wsum,
                                               int32_t* s_rs, int32_t* s_rsl, int32_t* s_roff, int32_t* s_anc) {
   const int4 ua = units[2 * u], ub = units[2 * u + 1];
@@ -1367,7 +1371,7 @@ __device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, cons
   const int l = lane(), w = threadIdx.x >> 6;
   const int tid = (int)threadIdx.x;
   // all global loads of the unit's tables first (one round trip)
-  int cnt = 0;
+  int cnt = 0, r0 = 0;
   int64_t src = 0;
   if (tid < 256) {  // <= 256 slices (parse workgroups) per table entry
     const int pw = ua.z + tid;
@@ -1375,6 +1379,7 @@ __device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, cons
       const int64_t slot = (int64_t)pw * nbs + v.bucket;
       cnt = bk_cnt[slot];
       src = rbase[pw] + bk_off[slot];
+      r0 = pwork[pw].y;
     }
   }
   const int64_t gg = (int64_t)v.gb + v.g0 + tid;
@@ -1395,6 +1400,7 @@ __device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, cons
     if (l == 63) s_wsum[w] = inc;
     s_pre[tid] = inc - cnt;
     s_src[tid] = src;
+    s_r0[tid] = r0;
   }
   __syncthreads();
   if (tid < 256) {
@@ -1439,7 +1445,8 @@ struct LeftArgs {
   const int64_t* up_off; const int32_t* sample; const int32_t* tstart;
   const int32_t* n_of; const int32_t* gbase;
   const int4* bc; const int4* units; const uint32_t* status;
-  const uint64_t* ins_sorted; const int32_t* bk_cnt; const int32_t* bk_off; const int64_t* rbase;
+  const uint32_t* ins_sorted; const int32_t* bk_cnt; const int32_t* bk_off; const int64_t* rbase;
+  const int4* pwork;  // parse work table {sample, r0, r1, 0}: a slice's first read
   int64_t N, read_offset, ovf_cap;
   int32_t nbs;
   const int32_t* right_start; const int32_t* rsl; const int32_t* roff; const int32_t* vals_out;
@@ -1456,6 +1463,7 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
   __shared__ uint32_t Ml[kBW * kMs];
   __shared__ int32_t s_pre[257];
   __shared__ int64_t s_src[256];
+  __shared__ int32_t s_r0[256];  // per slice: its parse workgroup's first read
   __shared__ int32_t s_wsum[4];
   __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1];  // per gap of the bucket (K_left)
   __shared__ uint32_t Tl[kBW * kTs];  // per (gap, run): inline bases [bi from the 3' end][code]
@@ -1466,11 +1474,13 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
     for (int k = threadIdx.x; k < kBW * kMs; k += blockDim.x) Ml[k] = 0;
     for (int k = threadIdx.x; k < kBW * kTs; k += blockDim.x) Tl[k] = 0;
     const UnitView uv = load_unit<false>(a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, a.right_start, a.rsl,
-                                         a.roff, nullptr, nullptr, nullptr, s_pre, s_src, s_wsum, s_rs, s_rsl, s_roff, nullptr);
+                                         a.roff, nullptr, nullptr, nullptr, a.pwork, s_r0, s_pre, s_src, s_wsum, s_rs,
+                                         s_rsl, s_roff, nullptr);
     const int n = uv.n;
     const int gb = uv.gb;
     const int g0 = uv.g0;
-    uint64_t evs[kEPT];
+    uint32_t evs[kEPT];
+    int32_t jsq[kEPT];  // slice of each event (its workgroup's first read)
     // all loads first (latency), then the tallies.  The thread's events move
     // kUB apart: with >= kUB events per slice on average (C3 / C4) its slice is
     // searched once, then advanced; with short slices (C2) every event's search
@@ -1480,9 +1490,11 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
 #pragma unroll
     for (int q = 0; q < kEPT; ++q) {
       const int e = uv.e0 + (int)threadIdx.x + q * kUB;
-      evs[q] = ~0ull;
+      evs[q] = ~0u;
+      jsq[q] = 0;
       if (e < uv.e0 + uv.cnt) {
         js = unit_slice_next(s_pre, e, adv ? js : -1);
+        jsq[q] = js;
         evs[q] = a.ins_sorted[s_src[js] + (e - s_pre[js])];
       }
     }
@@ -1495,11 +1507,11 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
     __syncthreads();
 #pragma unroll
     for (int q = 0; q < kEPT; ++q) {
-      const uint64_t ev = evs[q];
-      const int gap = (int)((ev >> 10) & kNullGap);
-      if (gap > n || gap < g0 || gap >= g0 + kBW) continue;
+      const uint32_t ev = evs[q];
+      if (ev == ~0u) continue;
+      const int gap = g0 + (int)((ev >> 10) & (kBW - 1));
       const int64_t g = (int64_t)gb + gap;
-      const int64_t rg = (int64_t)(ev >> 32);
+      const int64_t rg = a.read_offset + s_r0[jsq[q]] + (ev >> 16);
       const int L = (int)((ev >> 8) & 3u) + 1;
       const int p = gap - g0;
       const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
@@ -2251,7 +2263,7 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.cs_base = d.cs_base; a.ovf_cap = d.ovf_cap; a.read_offset = d.read_offset; a.n_reads = d.N;
   a.nbs = p->nbmax;
   a.i_end = d.i_end;
-  a.ins_raw = at<uint64_t>(p, mpc_plan::B_INSRAW); a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
+  a.ins_raw = at<uint64_t>(p, mpc_plan::B_INSRAW); a.ins_sorted = at<uint32_t>(p, mpc_plan::B_INSSORT);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
   a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.hasleft = d.hasleft; a.status = d.status;
@@ -2298,9 +2310,9 @@ static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
   LeftArgs a;
   a.up_off = d.up_off; a.sample = d.sample; a.tstart = d.tstart; a.n_of = d.n_of; a.gbase = d.gbase;
   a.bc = at<const int4>(p, mpc_plan::B_WBC); a.units = at<const int4>(p, mpc_plan::B_UNITS); a.status = d.status;
-  a.ins_sorted = at<uint64_t>(p, mpc_plan::B_INSSORT);
+  a.ins_sorted = at<uint32_t>(p, mpc_plan::B_INSSORT);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
-  a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
+  a.rbase = at<int64_t>(p, mpc_plan::B_RBASE); a.pwork = at<const int4>(p, mpc_plan::B_WPARSE);
   a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = p->nbmax;
   a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out; a.M = d.M; a.runt = d.runt;
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt;
@@ -2514,7 +2526,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_GBASE, p->S + 1, 4);
   set(mpc_plan::B_IEND, N, 4);
   set(mpc_plan::B_INSRAW, p->ins_cap, 8);
-  set(mpc_plan::B_INSSORT, p->ins_cap, 8);
+  set(mpc_plan::B_INSSORT, p->ins_cap, 4);
   set(mpc_plan::B_BKCNT, (int64_t)p->n_parse_wg * p->nbmax, 4);
   set(mpc_plan::B_BKOFF, (int64_t)p->n_parse_wg * p->nbmax, 4);
   set(mpc_plan::B_RBASE, p->n_parse_wg, 8);

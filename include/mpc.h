@@ -181,6 +181,7 @@ int mpc_run(mpc_plan* plan, double min_depth_factor, double global_threshold_fac
 #define MPC_K_LEFT 2
 #define MPC_K_FLANK 3
 #define MPC_K_INS 4  /* consumes (and zeroes) the run tallies K_left left: time it after a K_LEFT */
+#define MPC_K_RSORT 5 /* re-sorts the mixed RIGHT events of the last K_rsplit (idempotent) */
 int mpc_profile_kernel(mpc_plan* plan, int which, void* stream);
 
 #ifdef __cplusplus

@@ -1040,12 +1040,86 @@ __device__ __forceinline__ void rsplit_block(const Dev& d, int64_t b) {
 // K_rsort: the mixed RIGHT events (partial reads ending at gaps that also hold
 // LEFT events: few) sorted by (gap, read).  One workgroup: gather the per-block
 // lists of K_rsplit (in read order), then a stable LSD radix sort on the gap
-// (8-bit digits, wave multi-split ranks) -- in LDS when the list fits, else
-// ping-ponging through HBM (same code, generic pointers).
+// (8-bit digits, a contiguous segment per wave, wave multi-split ranks) -- in
+// LDS when the list fits, else ping-ponging through HBM (same code, generic
+// pointers).
 // ---------------------------------------------------------------------------
-constexpr int kRS = 1024;
 constexpr int kSortLds = 8192;
+constexpr int kRsuLds = 2;  // K_rsort chunks in flight in LDS (measured 1/2/4/8 at C1/C2/C4: 2)
 constexpr int kGatherLds = 2048;  // source blocks whose prefix stays in LDS (entry-parallel gather)
+
+// One stable LSD pass of K_rsort over digit (key >> sh) & 255: wave w owns the
+// contiguous segment [s0, s1) of the list (read order); per-wave digit
+// histograms, one scan -> per (wave, digit) start, then every wave walks ITS
+// segment in order, 64 entries at a time: stable ranks by wave multi-split,
+// the digit's cursor in the wave's own LDS row (no barrier inside the walk:
+// 4 per pass).  Force-inlined at call sites whose buffers are all LDS or all
+// HBM, so the accesses compile to ds_* / global_* instead of flat.
+constexpr int kRS = 1024;
+template <int U>  // chunks of 64 entries in flight per wave (HBM: latency; LDS: few)
+__device__ __forceinline__ void rsort_pass(const uint32_t* sk, const int32_t* sv, uint32_t* dk, int32_t* dv, int sh,
+                                           int64_t s0, int64_t s1, int32_t (*wc)[256], int32_t* hb) {
+  constexpr int NW = kRS / 64;
+  const int tid = threadIdx.x, l = lane(), w = tid >> 6;
+  const uint64_t lt = (1ull << l) - 1ull;
+  for (int k = l; k < 256; k += 64) wc[w][k] = 0;
+  for (int64_t i0 = s0; i0 < s1; i0 += U * 64) {
+    uint32_t kk[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + 64 * u + l;
+      kk[u] = i < s1 ? sk[i] : ~0u;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+      if (kk[u] != ~0u) atomicAdd(&wc[w][(kk[u] >> sh) & 255u], 1);
+  }
+  __syncthreads();
+  if (tid < 256) {
+    int t = 0;
+    for (int k = 0; k < NW; ++k) t += wc[k][tid];
+    hb[tid] = t;
+  }
+  __syncthreads();
+  if (tid < 64) {  // exclusive scan of the 256 digit totals (4 per lane)
+    const int x0 = hb[4 * tid], x1 = hb[4 * tid + 1], x2 = hb[4 * tid + 2], x3 = hb[4 * tid + 3];
+    const int t4 = x0 + x1 + x2 + x3;
+    const int e = wave_scan_i32(t4) - t4;
+    hb[4 * tid] = e; hb[4 * tid + 1] = e + x0; hb[4 * tid + 2] = e + x0 + x1; hb[4 * tid + 3] = e + x0 + x1 + x2;
+  }
+  __syncthreads();
+  if (tid < 256) {  // per (wave, digit) start: digit start + the digit's entries in lower waves
+    int run = hb[tid];
+    for (int k = 0; k < NW; ++k) { const int c = wc[k][tid]; wc[k][tid] = run; run += c; }
+  }
+  __syncthreads();
+  for (int64_t i0 = s0; i0 < s1; i0 += U * 64) {
+    uint32_t kk[U];
+    int32_t vv[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + 64 * u + l;
+      kk[u] = i < s1 ? sk[i] : 0u;
+      vv[u] = i < s1 ? sv[i] : 0;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const bool v = i0 + 64 * u + l < s1;
+      const uint32_t dg = (kk[u] >> sh) & 255u;
+      uint64_t m = ballot(v);
+#pragma unroll
+      for (int bit = 0; bit < 8; ++bit) {
+        const uint64_t bb = ballot(((dg >> bit) & 1u) != 0);
+        m &= ((dg >> bit) & 1u) ? bb : ~bb;
+      }
+      const int rank = __popcll(m & lt);
+      const int base = v ? wc[w][dg] : 0;
+      if (v) { dk[base + rank] = kk[u]; dv[base + rank] = vv[u]; }
+      if (v && rank == 0) wc[w][dg] = base + __popcll(m);  // after every lane's read (in order: one wave)
+    }
+  }
+  __syncthreads();
+}
 
 __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t end_bit) {
   __shared__ uint32_t lk[2][kSortLds];
@@ -1115,7 +1189,10 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
       const int64_t i = i0 + tid + (int64_t)u * kRS;
-      if (i < M) { kb[0][i] = kk[u]; vb[0][i] = vv[u]; }
+      if (i < M) {
+        if (in_lds) { lk[0][i] = kk[u]; lv[0][i] = vv[u]; }
+        else { kb[0][i] = kk[u]; vb[0][i] = vv[u]; }
+      }
     }
   }
   for (int b = tid; !pre_lds && b < nblocks; b += kRS) {
@@ -1138,49 +1215,16 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
     }
   }
   __syncthreads();
-  const uint64_t lt = (1ull << l) - 1ull;
-  for (int p = 0; p < passes; ++p) {
-    const int sh = 8 * p;
-    const uint32_t* sk = kb[p & 1];
-    const int32_t* sv = vb[p & 1];
-    uint32_t* dk = (in_lds && p == passes - 1) ? d.keys_out : kb[(p + 1) & 1];
-    int32_t* dv = (in_lds && p == passes - 1) ? d.vals_out : vb[(p + 1) & 1];
-    if (tid < 256) hb[tid] = 0;
-    __syncthreads();
-    for (int64_t i = tid; i < M; i += kRS) atomicAdd(&hb[(sk[i] >> sh) & 255u], 1);
-    __syncthreads();
-    if (tid < 64) {  // exclusive scan of the 256 digit counts (4 per lane)
-      const int x0 = hb[4 * tid], x1 = hb[4 * tid + 1], x2 = hb[4 * tid + 2], x3 = hb[4 * tid + 3];
-      const int t4 = x0 + x1 + x2 + x3;
-      const int e = wave_scan_i32(t4) - t4;
-      hb[4 * tid] = e; hb[4 * tid + 1] = e + x0; hb[4 * tid + 2] = e + x0 + x1; hb[4 * tid + 3] = e + x0 + x1 + x2;
-    }
-    __syncthreads();
-    for (int64_t t0 = 0; t0 < M; t0 += kRS) {  // stable multi-split, one tile of kRS entries
-      for (int k = tid; k < (kRS / 64) * 256; k += kRS) (&wc[0][0])[k] = 0;
-      const int64_t i = t0 + tid;
-      const bool v = i < M;
-      const uint32_t key = v ? sk[i] : 0u;
-      const int32_t val = v ? sv[i] : 0;
-      const uint32_t dg = (key >> sh) & 255u;
-      uint64_t m = ballot(v);
-#pragma unroll
-      for (int bit = 0; bit < 8; ++bit) {
-        const uint64_t bb = ballot(((dg >> bit) & 1u) != 0);
-        m &= ((dg >> bit) & 1u) ? bb : ~bb;
-      }
-      const int rank = __popcll(m & lt);
-      __syncthreads();
-      if (v && rank == 0) wc[w][dg] = __popcll(m);
-      __syncthreads();
-      if (tid < 256) {
-        int run = hb[tid];
-        for (int k = 0; k < kRS / 64; ++k) { const int c = wc[k][tid]; wc[k][tid] = run; run += c; }
-        hb[tid] = run;
-      }
-      __syncthreads();
-      if (v) { const int o = wc[w][dg] + rank; dk[o] = key; dv[o] = val; }
-      __syncthreads();
+  constexpr int NW = kRS / 64;
+  const int64_t s0 = M * w / NW, s1 = M * (w + 1) / NW;
+  if (in_lds) {  // LDS -> LDS passes, the last one LDS -> HBM
+    for (int p = 0; p + 1 < passes; ++p) rsort_pass<kRsuLds>(lk[p & 1], lv[p & 1], lk[(p + 1) & 1], lv[(p + 1) & 1], 8 * p, s0, s1, wc, hb);
+    rsort_pass<kRsuLds>(lk[(passes - 1) & 1], lv[(passes - 1) & 1], d.keys_out, d.vals_out, 8 * (passes - 1), s0, s1, wc, hb);
+  } else {
+    for (int p = 0; p < passes; ++p) {  // buffer (passes - p) & 1 is keys_out / vals_out: the last pass lands there
+      const bool src_out = ((passes - p) & 1) == 0;
+      rsort_pass<8>(src_out ? d.keys_out : d.keys_tmp, src_out ? d.vals_out : d.vals_tmp, src_out ? d.keys_tmp : d.keys_out,
+                 src_out ? d.vals_tmp : d.vals_out, 8 * p, s0, s1, wc, hb);
     }
   }
 }
@@ -2795,6 +2839,9 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
       break;
     case MPC_K_FLANK:
       hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(kFR), 0, st, flank_args(p, d));
+      break;
+    case MPC_K_RSORT:
+      hipLaunchKernelGGL(K_rsort, dim3(1), dim3(kRS), 0, st, d, (int32_t)((p->N + kRS - 1) / kRS), (int32_t)p->end_bit);
       break;
     default:
       return fail(MPC_E_ARG, "unknown kernel");

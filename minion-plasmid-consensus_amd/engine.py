@@ -23,7 +23,7 @@ PHASES = ("parse", "index", "runs", "tally", "layout", "rows")
 
 DE_NAMES = {DE_OP: "Unknown operator", DE_VALUE: "ValueError", DE_INDEX: "IndexError", DE_KEY: "KeyError",
             DE_CAPACITY: "row capacity", DE_INTERNAL: "internal invariant"}
-K_PARSE, K_ODD, K_LEFT, K_FLANK, K_INS = 0, 1, 2, 3, 4
+K_PARSE, K_ODD, K_LEFT, K_FLANK, K_INS, K_RSORT = 0, 1, 2, 3, 4, 5
 CS_PAD = 2048  # readable bytes required past the end of the cs buffer (mpc.h)
 FLANK_PAD = 16  # readable bytes required past the end of the up/down buffers (mpc.h)
 

@@ -198,7 +198,7 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
 // tallies): position within a kSubWin-position window << 2 | code, per wave and
 // window in the wave's region [(cs_off[ra] - cs_base) / 3 + 2 ra, ...) of window
 // w's slice (a '*' token takes 3 cs bytes); K_subs tallies them per window in LDS.
-constexpr int kSubWinBits = 13, kSubWin = 1 << kSubWinBits, kMaxSubWins = 8;
+constexpr int kSubWinBits = 14, kSubWin = 1 << kSubWinBits, kMaxSubWins = 4;
 
 __host__ __device__ inline int parse_hl_words(int n) { return (n + 1 + 31) / 32; }
 __host__ __device__ constexpr int parse_misc_bytes() { return kMaxPW * 4 + kMaxPW * 8; }
@@ -942,8 +942,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
 
 // ---------------------------------------------------------------------------
 // K_subs (tally mode 3): the substitution events of a sample's parse waves for
-// one kSubWin-position window, tallied in LDS (the event word IS the counter
-// index: position << 2 | code) and flushed with contiguous atomics.  One block
+// one kSubWin-position window, tallied in LDS as 16-bit counters (the event
+// word IS the counter index: position << 2 | code; a block's chunk holds at most
+// 65535 reads, and a read substitutes a position at most once) and flushed with
+// contiguous atomics.  One block
 // per (sample, window, chunk of <= kSubsWG parse workgroups); wave v walks the
 // chunk's regions v, v + 16, ... (8 loads in flight per lane).
 // ---------------------------------------------------------------------------
@@ -957,11 +959,11 @@ struct SubsArgs {
   int32_t nw_parse;
 };
 __global__ __launch_bounds__(1024) void K_subs(SubsArgs a) {
-  __shared__ uint32_t cnt[kSubWin * 4];
+  __shared__ uint32_t cnt[kSubWin * 2];  // (position, code pair): codes 2h | 2h+1 in the halves
   const int4 wk = a.work[blockIdx.x];
   const int smp = wk.x, win = wk.y, pw0 = wk.z, pw1 = wk.w;
   const int nreg = (pw1 - pw0) * a.nw_parse, l = lane(), v = threadIdx.x >> 6, nv = blockDim.x >> 6;
-  for (int k = threadIdx.x; k < kSubWin * 4; k += blockDim.x) cnt[k] = 0;
+  for (int k = threadIdx.x; k < kSubWin * 2; k += blockDim.x) cnt[k] = 0;
   __syncthreads();
   for (int rg = v; rg < nreg; rg += nv) {
     const int pw = pw0 + rg / a.nw_parse, ww = rg % a.nw_parse;
@@ -978,15 +980,15 @@ __global__ __launch_bounds__(1024) void K_subs(SubsArgs a) {
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u)
-        if (ev[u] != ~0u) atomicAdd(&cnt[ev[u]], 1u);
+        if (ev[u] != ~0u) atomicAdd(&cnt[ev[u] >> 1], 1u << (16 * (ev[u] & 1u)));
     }
   }
   __syncthreads();
   const int64_t p0 = (int64_t)win * kSubWin, n = a.n_of[smp];
   uint32_t* dst = a.sub + ((int64_t)a.gbase[smp] + p0) * 4;
-  for (int k = threadIdx.x; k < kSubWin * 4; k += blockDim.x) {  // consecutive lanes, consecutive words
-    const uint32_t x = cnt[k];
-    if (x && p0 + (k >> 2) < n) atomicAdd(dst + k, x);
+  for (int j = threadIdx.x; j < kSubWin * 4; j += blockDim.x) {  // consecutive lanes, consecutive words
+    const uint32_t x = (cnt[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+    if (x && p0 + (j >> 2) < n) atomicAdd(dst + j, x);
   }
 }
 
@@ -2546,7 +2548,8 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       int64_t pairs = 0;
       for (int s = 0; s < p->S; ++s)
         pairs += ((p->ref_len[s] + kSubWin - 1) / kSubWin) * (int64_t)(pw_begin[s + 1] - pw_begin[s]);
-      const int kc = (int)std::min<int64_t>(kSubsWG, std::max<int64_t>(1, (pairs + 255) / 256));
+      const int kc = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)kSubsWG, (pairs + 255) / 256,
+                                                                   65535 / std::max<int64_t>(1, p->max_wg_reads)}));
       for (int s = 0; s < p->S; ++s)
         for (int w = 0; w * (int64_t)kSubWin < p->ref_len[s]; ++w)
           for (int c = pw_begin[s]; c < pw_begin[s + 1]; c += kc)

@@ -45,10 +45,7 @@ constexpr int kInsInline = 4;       // insertions up to this length travel as on
 constexpr int kMaxRefLen = (1 << 20) - 2;  // 32-bit coordinates: advances are clamped at kAdvCap > n
 constexpr int kAdvCap = 1 << 20;    // > any reference length: a clamped advance keeps i past the end
 constexpr int kICap = 1 << 28;      // saturation of the running coordinate i
-#ifndef MPC_BW
-#define MPC_BW 64
-#endif
-constexpr int kBW = MPC_BW;         // gaps per insertion bucket (K_left workgroup)
+constexpr int kBW = 64;             // gaps per insertion bucket (K_left workgroup)
 static_assert(kBW <= 64 && (kBW & (kBW - 1)) == 0, "sorted insertion events hold the gap within its bucket in 6 bits");
 constexpr int kKMax = 8;            // runs per gap tallied in K_left's LDS (others go to HBM)
 constexpr uint32_t kNullGap = 0x3fffffu;
@@ -1313,16 +1310,10 @@ __device__ __forceinline__ int64_t run_left(const int32_t* rs, const int32_t* rs
 // K_units cuts every entry's events into units of <= kUnit events (hot
 // buckets become many units) and appends them to one list.
 // ---------------------------------------------------------------------------
-#ifndef MPC_UB
-#define MPC_UB 1024
-#endif
-#ifndef MPC_EPT
-#define MPC_EPT 16
-#endif
-constexpr int kUB = MPC_UB;           // threads of the unit kernels (K_left, K_ins)
+constexpr int kUB = 1024;             // threads of K_ins and of K_left's default geometry
 constexpr int kLeftVals = 4096;       // mixed RIGHT reads of a bucket staged in K_left's LDS
-constexpr int kEPT = MPC_EPT;         // events per thread per unit (loads batched)
-constexpr int kUnit = kUB * kEPT;     // events per work unit
+constexpr int kEPT = 16;         // events per thread per unit (loads batched)
+constexpr int kUnit = kUB * kEPT;     // events per work unit (K_left<kUB>; K_left<512>: half)
 
 struct UnitArgs {
   const int4* bc;  // {sample, bucket, pw0, pw1}
@@ -1330,6 +1321,7 @@ struct UnitArgs {
   const int32_t* bk_cnt; int4* units; uint32_t* status;  // units: 2 int4 per unit (see read_unit)
   int64_t n_bc, units_cap;
   int32_t nbs;
+  int32_t unit;  // events per work unit (K_left's threads x kEPT)
 };
 
 // kUE consecutive table entries per wave (one wave per entry at a time), one
@@ -1356,7 +1348,7 @@ __device__ __forceinline__ void units_block(const UnitArgs& a, int64_t blk) {
       t = wave_sum(t);
     }
     ts[e] = t;
-    nus[e] = (t + kUnit - 1) / kUnit;
+    nus[e] = (t + a.unit - 1) / a.unit;
     wsum += nus[e];
   }
   if (l == 0) s_wu[w] = wsum;
@@ -1378,9 +1370,9 @@ __device__ __forceinline__ void units_block(const UnitArgs& a, int64_t blk) {
     }
     const int n = a.n_of[bcs[e].x], gb = a.gbase[bcs[e].x];
     for (int i = l; i < nu; i += 64) {
-      const int e0 = i * kUnit;
+      const int e0 = i * a.unit;
       a.units[2 * (u0 + i)] = bcs[e];
-      a.units[2 * (u0 + i) + 1] = make_int4(e0, ts[e] - e0 < kUnit ? ts[e] - e0 : kUnit, n, gb);
+      a.units[2 * (u0 + i) + 1] = make_int4(e0, ts[e] - e0 < a.unit ? ts[e] - e0 : a.unit, n, gb);
     }
     u0 += nu;
   }
@@ -1500,7 +1492,8 @@ struct LeftArgs {
   const Ovf* ovf; const uint32_t* ovf_cnt;
 };
 
-__global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
+template <int UB>  // threads per block; work units of UB * kEPT events
+__global__ __launch_bounds__(UB) void K_left(LeftArgs a) {
   __shared__ int64_t s_key;
   __shared__ int32_t s_val;
   // strides padded to odd word counts: every gap of the bucket starts on a
@@ -1528,14 +1521,14 @@ __global__ __launch_bounds__(kUB) void K_left(LeftArgs a) {
     uint32_t evs[kEPT];
     int32_t jsq[kEPT];  // slice of each event (its workgroup's first read)
     // all loads first (latency), then the tallies.  The thread's events move
-    // kUB apart: with >= kUB events per slice on average (C3 / C4) its slice is
+    // UB apart: with >= UB events per slice on average (C3 / C4) its slice is
     // searched once, then advanced; with short slices (C2) every event's search
     // is independent (a chain of advancing searches would serialize them)
-    const bool adv = s_pre[256] >= kUB * uv.nsl;
+    const bool adv = s_pre[256] >= UB * uv.nsl;
     int js = -1;
 #pragma unroll
     for (int q = 0; q < kEPT; ++q) {
-      const int e = uv.e0 + (int)threadIdx.x + q * kUB;
+      const int e = uv.e0 + (int)threadIdx.x + q * UB;
       evs[q] = ~0u;
       jsq[q] = 0;
       if (e < uv.e0 + uv.cnt) {
@@ -2261,6 +2254,7 @@ struct mpc_plan {
   int64_t subev_cap = 0;
   int n_parse_wg = 0, parse_lds = 0, nbmax = 1, parse_win = 1024, parse_nw = 8;
   int64_t n_bc = 0, units_cap = 0, max_wg_reads = 0;
+  int32_t left_ub = 1024;  // K_left threads per block
   int32_t shard = 0, n_shards = 1;
   int tally_mode = 0;  // K_parse TM
   enum {
@@ -2380,10 +2374,17 @@ static UnitArgs unit_args(const mpc_plan* p, const Dev& d) {
   a.bc = at<const int4>(p, mpc_plan::B_WBC); a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT);
   a.units = at<int4>(p, mpc_plan::B_UNITS); a.status = d.status;
   a.n_of = d.n_of; a.gbase = d.gbase;
-  a.n_bc = p->n_bc; a.units_cap = p->units_cap; a.nbs = p->nbmax;
+  a.n_bc = p->n_bc; a.units_cap = p->units_cap; a.nbs = p->nbmax; a.unit = p->left_ub * kEPT;
   return a;
 }
+// K_left's geometry (planner: left_ub)
+static void launch_left(const mpc_plan* p, const Dev& d, hipStream_t st);
 static int64_t left_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 512)); }
+static LeftArgs left_args(const mpc_plan* p, const Dev& d);
+static void launch_left(const mpc_plan* p, const Dev& d, hipStream_t st) {
+  if (p->left_ub == 512) hipLaunchKernelGGL(K_left<512>, dim3(left_grid(p)), dim3(512), 0, st, left_args(p, d));
+  else hipLaunchKernelGGL(K_left<kUB>, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));
+}
 static int64_t ins_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 512)); }
 static int64_t flank_grid(const mpc_plan* p) { return std::max<int64_t>(1, (p->N + kFR - 1) / kFR); }
 
@@ -2573,7 +2574,18 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
           p->work_bc.insert(p->work_bc.end(), {s, b, c, std::min(c + 256, pw_begin[s + 1])});
     }
     p->n_bc = (int64_t)(p->work_bc.size() / 4);
-    p->units_cap = p->ins_cap / kUnit + p->n_bc + 1;
+    // K_left blocks of 512 threads (units of 8 k events) when there are many
+    // small insertion buckets: C5's 24 x 469 buckets of ~3 k events each are
+    // ~22 units per block in turn, whose fixed per-unit cost dominated at 1024
+    // threads (K_left 352 -> 287 us).  Few or large buckets (C1-C4) keep 1024
+    // (measured 4-45 % slower at 512: one unit per block, latency-bound).  The
+    // bucket size is estimated from the cs bytes per (sample, bucket)
+    {
+      int64_t nb_all = 0;
+      for (int s = 0; s < p->S; ++s) nb_all += (p->ref_len[s] + 1 + kBW - 1) / kBW;
+      p->left_ub = nb_all > 4 * 512 && in->cs_bytes / nb_all < (256 << 10) ? 512 : kUB;
+    }
+    p->units_cap = p->ins_cap / (p->left_ub * kEPT) + p->n_bc + 1;
   }
   const int64_t N = p->N, Ng = p->Ng, G = p->G, R = p->row_cap, RU = p->runs_cap;
   const int64_t nbg = (G + kGB - 1) / kGB, nbk = (R + kKB - 1) / kKB;
@@ -2791,7 +2803,7 @@ int mpc_tally(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));  // (units: mpc_index)
+  launch_left(p, d, st);  // (units: mpc_index)
   p->runt_dirty = true;  // until K_ins has mapped (and cleared) the run tallies
   HIPCHK(hipGetLastError());
   return MPC_OK;
@@ -2844,7 +2856,7 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
       launch_parse(p, d, st);
       break;
     case MPC_K_LEFT:
-      hipLaunchKernelGGL(K_left, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));
+      launch_left(p, d, st);
       p->runt_dirty = true;
       break;
     case MPC_K_INS:

@@ -4,6 +4,8 @@ import ctypes
 import os
 import re
 
+import pytest
+
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
@@ -66,3 +68,13 @@ def test_planner_geometry(pkg):
     assert st["max_reads_per_workgroup"] == st["reads_per_workgroup_cap"] == 16383
     for info in (c2, c3, c5, m6, st):
         assert info["parse_lds_bytes"] <= 160 * 1024 and info["parse_waves"] in (8, 12, 16)
+
+
+def test_planner_reference_limit(pkg):
+    """The largest reference the planner takes (mpc.h: 312,575 bases, tally mode
+    0 with 512-byte windows), and the error one base beyond it (host-only)."""
+    g = pkg.engine.geometry
+    info = g([312_575], [12], 312_575 * 3)
+    assert info["tally_mode"] == 0 and info["parse_lds_bytes"] <= 160 * 1024
+    with pytest.raises(pkg.engine.MpcError):
+        g([312_576], [12], 312_576 * 3)

@@ -93,19 +93,25 @@ SYNTH = [
     dict(n=50, n_reads=2000, profile="c1probe", seed=7, frac_partial=0.5, flank=(0, 8)),
     dict(n=3000, n_reads=500, profile="default", seed=9, frac_partial=0.3, ins_len=(1, 1500), del_len=(1, 1200),
          p_ins=0.0005, p_del=0.0005, flank=(0, 3000)),
-    # K_parse geometry by reference length: ~10 kb -> packed 10-byte LDS tallies
-    # (tally mode 2), ~20 kb -> LDS depth + global substitutions (mode 3),
+    # K_parse geometry by reference length (planner, mpc_plan_info): ~6 kb ->
+    # packed 10-byte LDS tallies (tally mode 2); 10-45 kb -> LDS depth +
+    # substitution events in 16384-position windows (mode 3: 1 and 3 windows);
     # ~70 kb -> global-atomic tallies (mode 0)
+    dict(n=6000, n_reads=1000, profile="default", seed=43, frac_partial=0.2),
     dict(n=10000, n_reads=1200, profile="indel", seed=44, frac_partial=0.2),
     dict(n=20000, n_reads=300, profile="default", seed=45, frac_partial=0.3),
+    dict(n=45000, n_reads=120, profile="indel", seed=47, frac_partial=0.3),
     dict(n=70000, n_reads=60, profile="default", seed=46, frac_partial=0.3),
 ]
+SYNTH_MODE = {6000: 2, 10000: 3, 20000: 3, 45000: 3, 70000: 0}
 
 
 @pytest.mark.parametrize("spec", SYNTH, ids=lambda s: f"n{s['n']}_N{s['n_reads']}_{s['profile']}_s{s['seed']}")
 def test_synthetic_full_pileup(pkg, spec):
     syn = pkg.synth.Synth(**spec)
     samples = [syn.sample(0), syn.sample(1)]
+    if spec["n"] in SYNTH_MODE:
+        assert pkg.engine.Plan(pkg.engine.Batch(samples)).info()["tally_mode"] == SYNTH_MODE[spec["n"]]
     for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0), (0.5, 2.5)):
         res = pkg.engine.pileup(samples, mdf, gtf)
         for s, (smp, r) in enumerate(zip(samples, res)):
@@ -217,3 +223,21 @@ def test_dense_tokens_match_oracle(pkg, seed):
     assert max(np.diff(smp["cs_off"])) > 2048  # reads span several windows
     for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
         _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("dense", seed, mdf))
+
+
+def test_max_reference_length(pkg):
+    """The longest reference one launch takes (include/mpc.h: 312,575 bases, the
+    planner's LDS budget for the parse state; 32-bit coordinates would allow
+    2^20 - 2): bit-exact full pileup at the limit, one base more is rejected."""
+    n = MAX_REF
+    syn = pkg.synth.Synth(n=n, n_reads=12, profile="default", seed=48, frac_partial=0.5, antisense=False)
+    smp = syn.sample(0)
+    assert len(smp["ref"]) == n
+    _cmp(pkg.engine.pileup([smp], -1.0, 1.0)[0], _oracle(smp, -1.0, 1.0), "max_ref")
+    long = dict(smp)
+    long["ref"] = np.concatenate([smp["ref"], np.frombuffer(b"A", dtype=np.uint8)])
+    with pytest.raises(pkg.engine.MpcError):
+        pkg.engine.Plan(pkg.engine.Batch([long]))
+
+
+MAX_REF = 312_575

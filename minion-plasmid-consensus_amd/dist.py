@@ -8,14 +8,16 @@ mapped_paf_read_parser.py:37-72, driven in PAF first-occurrence order :292).
 Everything else is an order-free integer tally.  See SURVEY.md 8(e).
 
 Every shard runs the phases of include/mpc.h on its own reads.  Between the
-phases it exchanges small per-gap / per-run arrays (no read data moves), four
+phases it exchanges small per-gap / per-run arrays (no read data moves), five
 collectives per step:
 
     after parse     OR      hasleft bitmap        (which gaps hold LEFT events)
     after index     GATHER  per-gap mixed RIGHT counts -> global run index space
-    after tally     MAX     over the workspace span MAXR | M | RUN_R
-                            (longest RIGHT string at RIGHT-only gaps, longest
-                            LEFT string per run, RIGHT string closing each run)
+    after tally     MAX     MAXR | M[:used] and RUN_R[:used], used = the runs
+                            in use (G + all shards' mixed RIGHT events, one host
+                            read after the gather): longest RIGHT string at
+                            RIGHT-only gaps, longest LEFT string per run, RIGHT
+                            string closing each run
     after rows      SUM     rows                  (every shard's rows hold its own
                             reads' counts, odd positions included)
 
@@ -177,8 +179,22 @@ def exchange_step(plans, ex, mdf, gtf, stream=None):
     ex.gather([p.buffer(eng.BUF_RIGHT_CNT, i32) for p in plans], [p.buffer(eng.BUF_RIGHT_CNT_ALL, i32) for p in plans])
     each("runs")
     each("tally")
-    # MAXR (RIGHT-only gaps), RUN_M, RUN_R: adjacent in the workspace, one MAX
-    ex.reduce([p.span(eng.BUF_MAXR, eng.BUF_RUN_R, i32) for p in plans], "max")
+    # MAXR (RIGHT-only gaps) and the USED runs of RUN_M / RUN_R: the run index
+    # space is sized for every read being a mixed RIGHT event (runs_cap = global
+    # reads + G: ~13 MB at C2 x 8 GPUs), the runs in use are G + all shards'
+    # mixed RIGHT events (~35 k there).  One host read of that count (after the
+    # gather it is on every shard), then two MAX reductions over the used parts
+    # (MAXR and RUN_M are adjacent in the workspace)
+    used = int(plans[0].buffer(eng.BUF_MAXR, i32).numel()) + int(plans[0].buffer(eng.BUF_RIGHT_CNT_ALL, i32).sum())
+    heads, tails = [], []
+    for p in plans:
+        span = p.span(eng.BUF_MAXR, eng.BUF_RUN_M, i32)
+        m = p.buffer(eng.BUF_RUN_M, i32)
+        moff = (m.data_ptr() - span.data_ptr()) // 4
+        heads.append(span[: moff + used])
+        tails.append(p.buffer(eng.BUF_RUN_R, i32)[:used])
+    ex.reduce(heads, "max")
+    ex.reduce(tails, "max")
     each("layout")
     each("rows")
     ex.reduce([p.buffer(eng.BUF_ROWS, i32) for p in plans], "sum")

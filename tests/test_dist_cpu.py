@@ -39,7 +39,9 @@ class FakePlan:
         self.buf = {
             eng.BUF_HASLEFT: i((G + 31) // 32 + 1, hi=2 ** 30),
             eng.BUF_DIFF: i(G), eng.BUF_SUB: i(4 * G),
-            eng.BUF_RIGHT_CNT: i(G, hi=50), eng.BUF_RIGHT_CNT_ALL: torch.zeros(n_shards * G, dtype=torch.int32),
+            # a few mixed RIGHT events: the runs in use (G + their sum) stop short of the run buffers' end
+            eng.BUF_RIGHT_CNT: i(G, hi=2) * (torch.arange(G) < 3).to(torch.int32),
+            eng.BUF_RIGHT_CNT_ALL: torch.zeros(n_shards * G, dtype=torch.int32),
             eng.BUF_MAXR: self.mx[:G], eng.BUF_RUN_M: self.mx[a:a + G + 11], eng.BUF_RUN_R: self.mx[b:b + G + 11],
             eng.BUF_ROWS: i(4 * ROWS),
         }
@@ -54,24 +56,42 @@ class FakePlan:
 
     def span(self, first, last, dtype):
         _, eng = _mod()
-        assert (first, last) == (eng.BUF_MAXR, eng.BUF_RUN_R)
-        return self.mx
+        assert (first, last) == (eng.BUF_MAXR, eng.BUF_RUN_M)
+        return self.mx[: G + 5 + G + 11]
 
 
 def expected(n_shards):
+    """(combined buffers, the combined used head of RUN_M / RUN_R, the runs in use)."""
     _, eng = _mod()
     plans = [FakePlan(k, n_shards) for k in range(n_shards)]
     init = [p.initial for p in plans]
     out = {}
     # DIFF / SUB stay per shard (every shard's rows carry its own odd-position counts)
-    for b, op in ((eng.BUF_HASLEFT, "or"), (eng.BUF_MAXR, "max"), (eng.BUF_RUN_M, "max"), (eng.BUF_RUN_R, "max"),
-                  (eng.BUF_ROWS, "sum")):
+    for b, op in ((eng.BUF_HASLEFT, "or"), (eng.BUF_MAXR, "max"), (eng.BUF_ROWS, "sum")):
         acc = init[0][b].clone()
         for x in init[1:]:
             acc = acc + x[b] if op == "sum" else (acc.maximum(x[b]) if op == "max" else acc | x[b])
         out[b] = acc
     out[eng.BUF_RIGHT_CNT_ALL] = torch.cat([x[eng.BUF_RIGHT_CNT] for x in init])
-    return out
+    # runs in use: G + all shards' mixed RIGHT events; the MAX covers only them
+    used = G + sum(int(x[eng.BUF_RIGHT_CNT].sum()) for x in init)
+    assert used < G + 11
+    heads = {}
+    for b in (eng.BUF_RUN_M, eng.BUF_RUN_R):
+        acc = init[0][b][:used].clone()
+        for x in init[1:]:
+            acc = acc.maximum(x[b][:used])
+        heads[b] = acc
+    return out, heads, used
+
+
+def _check(p, exp):
+    _, eng = _mod()
+    full, heads, used = exp
+    ok = all(torch.equal(p.buf[b], v) for b, v in full.items())
+    for b, v in heads.items():
+        ok = ok and torch.equal(p.buf[b][:used], v) and torch.equal(p.buf[b][used:], p.initial[b][used:])
+    return ok
 
 
 PHASES = ["parse", "index", "runs", "tally", "layout", "rows", "consensus"]
@@ -85,8 +105,7 @@ def test_local_exchange_combines():
     for p in plans:
         assert [x[0] for x in p.log] == PHASES
         assert p.log[-1] == ("consensus", 0.1, 5.0)
-        for b, v in exp.items():
-            assert torch.equal(p.buf[b], v), b
+        assert _check(p, exp)
         for b in (eng.BUF_RIGHT_CNT, eng.BUF_DIFF, eng.BUF_SUB):  # per-shard buffers untouched
             assert torch.equal(p.buf[b], p.initial[b]), b
 
@@ -121,9 +140,7 @@ def _worker(rank, world, port, q):
         plan = FakePlan(rank, world)
         dist.exchange_step([plan], ex, 0.5, 2.5)
         exp = expected(world)
-        ok = [x[0] for x in plan.log] == PHASES
-        for b, v in exp.items():
-            ok = ok and torch.equal(plan.buf[b], v)
+        ok = [x[0] for x in plan.log] == PHASES and _check(plan, exp)
         sizes = ex.sizes([10 + rank])
         mx = ex.max_int([rank * 7])
         q.put((rank, bool(ok), sizes, mx))

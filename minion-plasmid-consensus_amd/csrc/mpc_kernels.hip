@@ -1869,7 +1869,7 @@ __device__ __forceinline__ int code_exact(uint32_t c) {
   return c == expect ? code : -1;
 }
 
-constexpr int kStageB = 8192;  // flank bytes staged in LDS per chunk (a block's range is processed in chunks)
+constexpr int kStageB = 16384;  // flank bytes staged in LDS per chunk (a block's range is processed in chunks; C2: 1 per side)
 
 // Byte-parallel: the block's flank bytes (both sides) are staged in LDS chunk by
 // chunk; every thread takes 4 consecutive bytes.  The owner of a byte is found

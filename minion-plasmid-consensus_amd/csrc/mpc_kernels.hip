@@ -526,8 +526,7 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, int64
 
 // Workgroup = contiguous reads of ONE sample (host work table); wave w takes
 // the w-th part of them and streams their cs bytes in windows of WIN bytes
-// (WIN/64 per lane, coalesced; the next window is loaded while this one is
-// processed).  Token boundaries (special characters and read starts) are bits
+// (WIN/64 per lane, coalesced).  Token boundaries (special characters and read starts) are bits
 // of an LDS mask.  A window is cut at its LAST boundary C, so every token in
 // [P, C) ends inside the window (no lookahead halo); the next window starts at
 // C.  The token starts are compacted into a list of UNITS -- a ':' token
@@ -704,10 +703,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       W.s_read[q] = (int32_t)(rs0 + l);
       W.s_iend[q] = (ts < 0 ? 0 : (ts > n ? n + 1 : ts)) | (dn ? 1 << 30 : 0);
     }
-    // ---- prefetch the next window ----
+    // ---- the next window starts at C (its loads are issued after this
+    // window's rounds: holding them across the rounds cost 12 VGPRs and bought
+    // nothing, the other 15 waves hide the latency) ----
     const int64_t Pn = C, rsn = rs0 + nst;
-    WinIn<CH> nxt;
-    if (Pn < wend) nxt = fetch_window<CH>(a, Pn, rsn, l);
     // ---- token list: starts in [P, C) (bit 15 = read start), then the sentinel ----
     int T;
     {
@@ -921,7 +920,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     wave_sync_lds();
     P = Pn;
     rs0 = rsn;
-    if (Pn < wend) cur = nxt;
+    if (Pn < wend) cur = fetch_window<CH>(a, Pn, rsn, l);
   }
   // reads starting at the range end have an empty cs
   for (int64_t r = rs0 + l; r < rb; r += 64) {

@@ -1491,8 +1491,11 @@ struct LeftArgs {
   const Ovf* ovf; const uint32_t* ovf_cnt;
 };
 
+// UB = 1024: at most 64 VGPRs, so two 16-wave blocks share a CU (LDS ~57 KB
+// each): the per-unit latency chain overlaps (C3 K_left 312 -> 227 us, C4
+// 387 -> 286 us; 5 VGPRs spill)
 template <int UB>  // threads per block; work units of UB * kEPT events
-__global__ __launch_bounds__(UB) void K_left(LeftArgs a) {
+__global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ? 8 : 4))) void K_left(LeftArgs a) {
   __shared__ int64_t s_key;
   __shared__ int32_t s_val;
   // strides padded to odd word counts: every gap of the bucket starts on a

@@ -1491,11 +1491,12 @@ struct LeftArgs {
   const Ovf* ovf; const uint32_t* ovf_cnt;
 };
 
-// UB = 1024: at most 64 VGPRs, so two 16-wave blocks share a CU (LDS ~57 KB
-// each): the per-unit latency chain overlaps (C3 K_left 312 -> 227 us, C4
-// 387 -> 286 us; 5 VGPRs spill)
+// Resident blocks per CU, so that the per-unit latency chains overlap:
+// UB = 1024 at most 64 VGPRs, two 16-wave blocks (LDS ~57 KB each; C3 K_left
+// 312 -> 227 us, C4 387 -> 286 us; 5 VGPRs spill); UB = 512 at most 80 VGPRs
+// and a smaller RIGHT-read stage, three 8-wave blocks (C5 285 -> 218 us)
 template <int UB>  // threads per block; work units of UB * kEPT events
-__global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ? 8 : 4))) void K_left(LeftArgs a) {
+__global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ? 8 : 6))) void K_left(LeftArgs a) {
   __shared__ int64_t s_key;
   __shared__ int32_t s_val;
   // strides padded to odd word counts: every gap of the bucket starts on a
@@ -1508,7 +1509,9 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
   __shared__ int32_t s_wsum[4];
   __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1];  // per gap of the bucket (K_left)
   __shared__ uint32_t Tl[kBW * kTs];  // per (gap, run): inline bases [bi from the 3' end][code]
-  __shared__ int32_t s_vals[kLeftVals];   // the bucket's mixed RIGHT reads (vals_out), searched per event
+  // 512-thread blocks: a smaller stage, so three blocks fit a CU's LDS
+  constexpr int kLV = UB == 512 ? 3072 : kLeftVals;
+  __shared__ int32_t s_vals[kLV];         // the bucket's mixed RIGHT reads (vals_out), searched per event
   // (K_units raises DE_INTERNAL instead of overrunning the unit list)
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
@@ -1543,7 +1546,7 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     // stage the bucket's (contiguous in vals_out) in LDS, so no event waits on
     // a chain of dependent global loads
     const int32_t v0 = s_rsl[0], vn = s_rsl[uv.gl + 1 - g0] - v0;
-    const bool vl = vn <= kLeftVals;
+    const bool vl = vn <= kLV;
     for (int k = threadIdx.x; vl && k < vn; k += blockDim.x) s_vals[k] = a.vals_out[v0 + k];
     __syncthreads();
 #pragma unroll
@@ -2381,7 +2384,10 @@ static UnitArgs unit_args(const mpc_plan* p, const Dev& d) {
 }
 // K_left's geometry (planner: left_ub)
 static void launch_left(const mpc_plan* p, const Dev& d, hipStream_t st);
-static int64_t left_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 512)); }
+// two (1024-thread) or three (512-thread) resident blocks per CU
+static int64_t left_grid(const mpc_plan* p) {
+  return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, p->left_ub == 512 ? 768 : 512));
+}
 static LeftArgs left_args(const mpc_plan* p, const Dev& d);
 static void launch_left(const mpc_plan* p, const Dev& d, hipStream_t st) {
   if (p->left_ub == 512) hipLaunchKernelGGL(K_left<512>, dim3(left_grid(p)), dim3(512), 0, st, left_args(p, d));

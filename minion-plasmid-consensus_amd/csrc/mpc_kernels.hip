@@ -2097,7 +2097,7 @@ __device__ __forceinline__ uint4 call_slot(uint4 cv, double gtf, uint32_t* total
 
 // calls of every row + max depth over slot 0 (:332-341); rows t + 256 k of the block
 template <int kCR>
-__global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K_call(Dev d, int64_t R) {
   constexpr int kCB = 256 * kCR;  // rows per block
   __shared__ int32_t srow[kSmpLds];
   __shared__ int32_t s_blk[2], s_w[4];
@@ -2154,7 +2154,7 @@ __global__ __launch_bounds__(256) void K_call(Dev d, int64_t R) {
 
 // keep[row] = emitted (:428) and per-block counts (kKB rows per block)
 constexpr int kKB = 1024;  // rows per K_keep / K_emit block (4 per thread)
-__global__ __launch_bounds__(256) void K_keep(Dev d, int64_t R) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K_keep(Dev d, int64_t R) {
   __shared__ int32_t srow[kSmpLds];
   __shared__ int32_t s_w[4];
   load_sample_rows(d, srow);
@@ -2180,7 +2180,7 @@ __global__ __launch_bounds__(256) void K_keep(Dev d, int64_t R) {
   if (threadIdx.x == 0) d.ksum[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
 }
 
-__global__ __launch_bounds__(256) void K_emit(Dev d, int64_t R) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K_emit(Dev d, int64_t R) {
   __shared__ int32_t s_red[4], s_w[4];
   __shared__ int32_t srow[kSmpLds];
   load_sample_rows(d, srow);  // (ordered before use by the barriers below)

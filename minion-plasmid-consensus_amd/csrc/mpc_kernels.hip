@@ -820,10 +820,13 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       uint32_t pk = codes;
       pk = (pk | (pk >> 6)) & 0x000f000fu;
       pk = (pk | (pk >> 12)) & 0xffu;
-      uint32_t pay = star ? ((codes >> shl) & 3u) : (pk & ((1u << (2 * ol4)) - 1u));
+      const uint32_t mstar = 0u - (uint32_t)star;
+      uint32_t pay = (mstar & ((codes >> shl) & 3u)) | (~mstar & (pk & ((1u << (2 * ol4)) - 1u)));
       const bool slow = lfar | (pre & !cdig) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));
-      int kind = !act ? 0 : colon ? (adv_c > 0 ? 1 : 0) : (olen <= 0) ? 0 : star ? 2 : plus ? 3 : minus ? 4 : 0;
-      int adv = kind == 1 ? adv_c : kind == 2 ? 1 : kind == 4 ? (olen < kAdvCap ? olen : kAdvCap) : 0;
+      const int kop = ((int)star << 1) | ((int)plus * 3) | ((int)minus << 2);  // exclusive classes
+      const int mcol = -(int)colon;
+      int kind = (-(int)act) & ((mcol & (int)(adv_c > 0)) | (~mcol & (-(int)(olen > 0) & kop)));
+      int adv = (-(int)(kind == 1) & adv_c) | (int)(kind == 2) | (-(int)(kind == 4) & (olen < kAdvCap ? olen : kAdvCap));
       uint32_t err = (v & !spec) ? DE_OP : 0u;  // cs does not start with an operator (:100-102)
       if (act & star & (olen == 0)) err |= DE_INDEX;  // operand[-1] of '' (:96)
       if ((kind == 2) & !last_ok) err |= DE_KEY;

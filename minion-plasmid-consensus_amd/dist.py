@@ -163,9 +163,12 @@ def shard_layout(n_reads_per_shard):
     return [int(o) for o in offs[:-1]], int(offs[-1])
 
 
-def exchange_step(plans, ex, mdf, gtf, stream=None):
+def exchange_step(plans, ex, mdf, gtf, stream=None, used=None):
     """One global pileup over the shards in ``plans`` (all of this process's
-    shards; with DistExchange exactly one).  Collective: every shard must call it."""
+    shards; with DistExchange exactly one).  Collective: every shard must call it.
+    ``used`` (the runs in use, see below) is a property of the shards' reads:
+    a caller that steps the same batches again passes the value this function
+    returned for them, and the step then has no host synchronisation."""
     import torch
     i32 = torch.int32
 
@@ -185,7 +188,8 @@ def exchange_step(plans, ex, mdf, gtf, stream=None):
     # mixed RIGHT events (~35 k there).  One host read of that count (after the
     # gather it is on every shard), then two MAX reductions over the used parts
     # (MAXR and RUN_M are adjacent in the workspace)
-    used = int(plans[0].buffer(eng.BUF_MAXR, i32).numel()) + int(plans[0].buffer(eng.BUF_RIGHT_CNT_ALL, i32).sum())
+    if used is None:
+        used = int(plans[0].buffer(eng.BUF_MAXR, i32).numel()) + int(plans[0].buffer(eng.BUF_RIGHT_CNT_ALL, i32).sum())
     heads, tails = [], []
     for p in plans:
         span = p.span(eng.BUF_MAXR, eng.BUF_RUN_M, i32)
@@ -199,6 +203,7 @@ def exchange_step(plans, ex, mdf, gtf, stream=None):
     each("rows")
     ex.reduce([p.buffer(eng.BUF_ROWS, i32) for p in plans], "sum")
     each("consensus", mdf, gtf)
+    return used
 
 
 class ShardedPileup:
@@ -229,6 +234,7 @@ class ShardedPileup:
         cap = self.ex.max_int([cap] * local)[0] if isinstance(self.ex, DistExchange) else cap
         self.plans = [eng.Plan(b, cap) for b in self.batches]
         self._sized = False
+        self._used = None
 
     # bench.py interface (one local shard)
     @property
@@ -240,7 +246,9 @@ class ShardedPileup:
         return self.plans[0]
 
     def step(self, mdf, gtf, stream=None):
-        exchange_step(self.plans, self.ex, mdf, gtf, stream)
+        # the runs in use depend only on the reads: read back once, reused by
+        # later steps over the same batches (no host sync inside a step)
+        used = exchange_step(self.plans, self.ex, mdf, gtf, stream, self._used)
         if not self._sized:
             # the layout (and so the row count) is identical on every shard
             st = self.plans[0].status()
@@ -249,8 +257,9 @@ class ShardedPileup:
             if flags & eng.DE_CAPACITY:
                 need = int(st[eng.MPC_ST_ROWS_NEEDED]) + 16
                 self.plans = [eng.Plan(b, need) for b in self.batches]
-                exchange_step(self.plans, self.ex, mdf, gtf, stream)
+                used = exchange_step(self.plans, self.ex, mdf, gtf, stream)
             self._sized = True
+            self._used = used
 
     def check(self):
         for p in self.plans:

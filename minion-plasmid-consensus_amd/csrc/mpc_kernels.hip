@@ -108,6 +108,7 @@ struct Dev {  // device-side views of the plan for the small kernels (passed by 
   uint32_t* rows; uint8_t* meta; int64_t row_cap;
   uint32_t* runt;                    // [Ng+G][4][4] per run: inline insertion bases by slot from the right end
   uint32_t* res; int32_t* keep; int32_t* ksum; uint32_t* calls; int32_t* ncalls; uint32_t* maxdepth;
+  int32_t* srow;                     // [S] first row of every sample (K_assemble)
   double mdf, gtf;
 };
 
@@ -1732,7 +1733,6 @@ __global__ __launch_bounds__(kGB) void K_assemble(Dev d) {
   const int64_t rb = (int64_t)pre.x + wr + ir - rc;  // exclusive
   const int64_t dep = (int64_t)pre.y + wd + id;      // inclusive
   d.row_base[g] = (int32_t)rb;
-  if (tot > d.row_cap) return;
   int lo_s = 0, hi_s = d.S - 1;
   while (lo_s < hi_s) {
     const int mid = (lo_s + hi_s + 1) >> 1;
@@ -1740,6 +1740,8 @@ __global__ __launch_bounds__(kGB) void K_assemble(Dev d) {
   }
   const int s = lo_s;
   const int64_t p = g - d.gbase[s];
+  if (p == 0) d.srow[s] = (int32_t)rb;  // the consensus kernels' sample table (one load, no gbase chain)
+  if (tot > d.row_cap) return;
   const int64_t n = d.n_of[s];
   const int64_t nslots = (int64_t)rc - (p < n ? 1 : 0);
   if (nslots > 0) d.meta[rb] = 2;  // first slot of the gap
@@ -2045,7 +2047,7 @@ __device__ __forceinline__ int sample_of_row(const Dev& d, int64_t row) {
   int lo = 0, hi = d.S - 1;  // last sample whose first row <= row
   while (lo < hi) {
     const int mid = (lo + hi + 1) >> 1;
-    if (d.row_base[d.gbase[mid]] <= row) lo = mid; else hi = mid - 1;
+    if (d.srow[mid] <= row) lo = mid; else hi = mid - 1;
   }
   return lo;
 }
@@ -2053,7 +2055,7 @@ __device__ __forceinline__ int sample_of_row(const Dev& d, int64_t row) {
 // first row of every sample in LDS (kSmpLds samples; beyond that the global search)
 constexpr int kSmpLds = 512;
 __device__ __forceinline__ void load_sample_rows(const Dev& d, int32_t* srow) {
-  for (int s = threadIdx.x; s < d.S && s < kSmpLds; s += blockDim.x) srow[s] = d.row_base[d.gbase[s]];
+  for (int s = threadIdx.x; s < d.S && s < kSmpLds; s += blockDim.x) srow[s] = d.srow[s];
 }
 __device__ __forceinline__ int sample_of_row_lds(const Dev& d, const int32_t* srow, int64_t row) {
   if (d.S > kSmpLds) return sample_of_row(d, row);
@@ -2117,11 +2119,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K
   uint4 cv[kCR];
   uint8_t mt[kCR];
 #pragma unroll
-  for (int k = 0; k < kCR; ++k) {  // all loads first
+  for (int k = 0; k < kCR; ++k) {  // all loads first (in bounds: rows < R), in parallel with the status word
     const int64_t row = b0 + threadIdx.x + 256 * k;
-    cv[k] = row < need ? reinterpret_cast<const uint4*>(d.rows)[row] : make_uint4(0, 0, 0, 0);
-    mt[k] = row < need ? d.meta[row] : 0;
+    cv[k] = row < R ? reinterpret_cast<const uint4*>(d.rows)[row] : make_uint4(0, 0, 0, 0);
+    mt[k] = row < R ? d.meta[row] : 0;
   }
+#pragma unroll
+  for (int k = 0; k < kCR; ++k)
+    if (b0 + threadIdx.x + 256 * k >= need) { cv[k] = make_uint4(0, 0, 0, 0); mt[k] = 0; }
   __syncthreads();
   int32_t dep[kCR];  // slot-0 depth of the row (:336), -1: none
 #pragma unroll
@@ -2159,8 +2164,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K
 constexpr int kKB = 1024;  // rows per K_keep / K_emit block (4 per thread)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K_keep(Dev d, int64_t R) {
   __shared__ int32_t srow[kSmpLds];
+  __shared__ uint32_t smd[kSmpLds];
   __shared__ int32_t s_w[4];
   load_sample_rows(d, srow);
+  for (int s = threadIdx.x; s < d.S && s < kSmpLds; s += blockDim.x) smd[s] = d.maxdepth[s];
   const int64_t base = (int64_t)blockIdx.x * kKB + 4 * threadIdx.x;
   uint4 v[4];
 #pragma unroll
@@ -2172,7 +2179,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K
   for (int k = 0; k < 4; ++k) {
     if (v[k].x >> 24) {
       const int s = sample_of_row_lds(d, srow, base + k);
-      const double thr = (double)d.maxdepth[s] * d.mdf;  // :338
+      const double thr = (double)(s < kSmpLds ? smd[s] : d.maxdepth[s]) * d.mdf;  // :338
       if ((double)v[k].y > thr) { ++c; bits |= 1u << k; }  // :428
     }
   }
@@ -2222,7 +2229,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K
   // ncalls[s] = calls before the first row of sample s; ncalls[S] = all
   const int64_t b0 = (int64_t)blockIdx.x * kKB;
   for (int s = 0; s < d.S; ++s) {
-    const int64_t rb = s < kSmpLds ? srow[s] : d.row_base[d.gbase[s]];
+    const int64_t rb = s < kSmpLds ? srow[s] : d.srow[s];
     if (rb >= b0 && rb < b0 + kKB && (rb - b0) / 4 == threadIdx.x) {
       int64_t q = pre + wpre + inc - c;
       for (int k = 0; k < (int)((rb - b0) & 3); ++k) q += (bits >> k) & 1u;
@@ -2270,7 +2277,7 @@ struct mpc_plan {
     B_HASLEFT, B_KIN, B_VIN, B_KOUT, B_VOUT, B_KTMP, B_VTMP, B_BCNT, B_BPRE, B_RLEN, B_RPOS, B_RSTART, B_RSLOC, B_ROFF, B_RCNT, B_RCNTALL,
     // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
     B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
-    B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_WPARSE, B_WBC, B_UNITS, B_RUNT,
+    B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_SROW, B_WPARSE, B_WBC, B_UNITS, B_RUNT,
     B_SUBEV, B_SUBCNT, B_WSUB, B_COUNT
   };
   size_t off[B_COUNT];
@@ -2310,6 +2317,7 @@ Dev mpc_plan::dev() const {
   d.row_cap = row_cap;
   d.res = at<uint32_t>(this, B_RES); d.keep = at<int32_t>(this, B_KEEP); d.ksum = at<int32_t>(this, B_KSUM);
   d.calls = at<uint32_t>(this, B_CALLS); d.ncalls = at<int32_t>(this, B_NCALLS); d.maxdepth = at<uint32_t>(this, B_MAXD);
+  d.srow = at<int32_t>(this, B_SROW);
   return d;
 }
 
@@ -2648,6 +2656,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_CALLS, R * 4, 4);
   set(mpc_plan::B_NCALLS, p->S + 1, 4);
   set(mpc_plan::B_MAXD, p->S, 4);
+  set(mpc_plan::B_SROW, p->S, 4);
   set(mpc_plan::B_WPARSE, (int64_t)p->work_parse.size(), 4);
   set(mpc_plan::B_WBC, (int64_t)p->work_bc.size(), 4);
   set(mpc_plan::B_UNITS, p->units_cap * 8, 4);  // 2 int4 per unit

@@ -8,16 +8,17 @@ mapped_paf_read_parser.py:37-72, driven in PAF first-occurrence order :292).
 Everything else is an order-free integer tally.  See SURVEY.md 8(e).
 
 Every shard runs the phases of include/mpc.h on its own reads.  Between the
-phases it exchanges small per-gap / per-run arrays (no read data moves), five
+phases it exchanges small per-gap / per-run arrays (no read data moves), four
 collectives per step:
 
     after parse     OR      hasleft bitmap        (which gaps hold LEFT events)
     after index     GATHER  per-gap mixed RIGHT counts -> global run index space
-    after tally     MAX     MAXR | M[:used] and RUN_R[:used], used = the runs
-                            in use (G + all shards' mixed RIGHT events, one host
-                            read after the gather): longest RIGHT string at
-                            RIGHT-only gaps, longest LEFT string per run, RIGHT
-                            string closing each run
+    after tally     MAX     MAXR | M[:used] | RUN_R[:used] (RUN_R parked in M's
+                            unused tail: one reduction), used = the runs in use
+                            (G + all shards' mixed RIGHT events, read on the host
+                            once per batch): longest RIGHT string at RIGHT-only
+                            gaps, longest LEFT string per run, RIGHT string
+                            closing each run
     after rows      SUM     rows                  (every shard's rows hold its own
                             reads' counts, odd positions included)
 
@@ -190,15 +191,26 @@ def exchange_step(plans, ex, mdf, gtf, stream=None, used=None):
     # (MAXR and RUN_M are adjacent in the workspace)
     if used is None:
         used = int(plans[0].buffer(eng.BUF_MAXR, i32).numel()) + int(plans[0].buffer(eng.BUF_RIGHT_CNT_ALL, i32).sum())
-    heads, tails = [], []
+    heads, tails, parked = [], [], []
     for p in plans:
         span = p.span(eng.BUF_MAXR, eng.BUF_RUN_M, i32)
         m = p.buffer(eng.BUF_RUN_M, i32)
         moff = (m.data_ptr() - span.data_ptr()) // 4
-        heads.append(span[: moff + used])
-        tails.append(p.buffer(eng.BUF_RUN_R, i32)[:used])
+        rr = p.buffer(eng.BUF_RUN_R, i32)[:used]
+        if 2 * used <= m.numel():
+            # ONE max: RUN_R[:used] parked in RUN_M's unused tail [used, 2 used)
+            # (no kernel reads runs >= used; the next clear zeroes it)
+            m[used: 2 * used].copy_(rr)
+            heads.append(span[: moff + 2 * used])
+            parked.append((m[used: 2 * used], rr))
+        else:
+            heads.append(span[: moff + used])
+            tails.append(rr)
     ex.reduce(heads, "max")
-    ex.reduce(tails, "max")
+    if tails:
+        ex.reduce(tails, "max")
+    for src, dst in parked:
+        dst.copy_(src)
     each("layout")
     each("rows")
     ex.reduce([p.buffer(eng.BUF_ROWS, i32) for p in plans], "sum")

@@ -29,20 +29,22 @@ def _mod():
 class FakePlan:
     """Exchange buffers of one shard, seeded per shard; phases are recorded."""
 
-    def __init__(self, shard, n_shards):
+    def __init__(self, shard, n_shards, mlen=G + 11):
         _, eng = _mod()
         rng = np.random.default_rng(1000 + shard)
         i = lambda *shape, hi=1000: torch.from_numpy(rng.integers(0, hi, size=shape).astype(np.int32))
-        # MAXR, RUN_M, RUN_R: one workspace span with padding between them (include/mpc.h)
-        self.mx = i(G + 5 + (G + 11) + 3 + (G + 11))
-        a, b = G + 5, 2 * G + 16 + 3
+        # MAXR, RUN_M, RUN_R: one workspace span with padding between them (include/mpc.h);
+        # mlen >= 2 x the runs in use: RUN_R is reduced parked in RUN_M's tail (one MAX)
+        self.mlen = mlen
+        self.mx = i(G + 5 + mlen + 3 + mlen)
+        a, b = G + 5, G + 5 + mlen + 3
         self.buf = {
             eng.BUF_HASLEFT: i((G + 31) // 32 + 1, hi=2 ** 30),
             eng.BUF_DIFF: i(G), eng.BUF_SUB: i(4 * G),
             # a few mixed RIGHT events: the runs in use (G + their sum) stop short of the run buffers' end
             eng.BUF_RIGHT_CNT: i(G, hi=2) * (torch.arange(G) < 3).to(torch.int32),
             eng.BUF_RIGHT_CNT_ALL: torch.zeros(n_shards * G, dtype=torch.int32),
-            eng.BUF_MAXR: self.mx[:G], eng.BUF_RUN_M: self.mx[a:a + G + 11], eng.BUF_RUN_R: self.mx[b:b + G + 11],
+            eng.BUF_MAXR: self.mx[:G], eng.BUF_RUN_M: self.mx[a:a + mlen], eng.BUF_RUN_R: self.mx[b:b + mlen],
             eng.BUF_ROWS: i(4 * ROWS),
         }
         self.initial = {k: v.clone() for k, v in self.buf.items()}
@@ -57,13 +59,13 @@ class FakePlan:
     def span(self, first, last, dtype):
         _, eng = _mod()
         assert (first, last) == (eng.BUF_MAXR, eng.BUF_RUN_M)
-        return self.mx[: G + 5 + G + 11]
+        return self.mx[: G + 5 + self.mlen]
 
 
-def expected(n_shards):
+def expected(n_shards, mlen=G + 11):
     """(combined buffers, the combined used head of RUN_M / RUN_R, the runs in use)."""
     _, eng = _mod()
-    plans = [FakePlan(k, n_shards) for k in range(n_shards)]
+    plans = [FakePlan(k, n_shards, mlen) for k in range(n_shards)]
     init = [p.initial for p in plans]
     out = {}
     # DIFF / SUB stay per shard (every shard's rows carry its own odd-position counts)
@@ -90,18 +92,24 @@ def _check(p, exp):
     full, heads, used = exp
     ok = all(torch.equal(p.buf[b], v) for b, v in full.items())
     for b, v in heads.items():
-        ok = ok and torch.equal(p.buf[b][:used], v) and torch.equal(p.buf[b][used:], p.initial[b][used:])
+        ok = ok and torch.equal(p.buf[b][:used], v)
+        if b == eng.BUF_RUN_M and 2 * used <= p.mlen:  # RUN_R's reduced head parked behind the used runs
+            ok = ok and torch.equal(p.buf[b][used: 2 * used], heads[eng.BUF_RUN_R])
+            ok = ok and torch.equal(p.buf[b][2 * used:], p.initial[b][2 * used:])
+        else:
+            ok = ok and torch.equal(p.buf[b][used:], p.initial[b][used:])
     return ok
 
 
 PHASES = ["parse", "index", "runs", "tally", "layout", "rows", "consensus"]
 
 
-def test_local_exchange_combines():
+@pytest.mark.parametrize("mlen", [G + 11, 3 * G])  # two MAX reductions / one (RUN_R parked in RUN_M)
+def test_local_exchange_combines(mlen):
     dist, eng = _mod()
-    plans = [FakePlan(k, 3) for k in range(3)]
+    plans = [FakePlan(k, 3, mlen) for k in range(3)]
     dist.exchange_step(plans, dist.LocalExchange(), 0.1, 5.0)
-    exp = expected(3)
+    exp = expected(3, mlen)
     for p in plans:
         assert [x[0] for x in p.log] == PHASES
         assert p.log[-1] == ("consensus", 0.1, 5.0)

@@ -12,8 +12,10 @@ procs = []
 for arg in sys.argv[1:]:
     name, sets = arg.split("=") if "=" in arg else (arg, arg)
     s = open(SRC).read()
+    flags = []
     for ps in sets.split("+"):
         if ps == "base": continue
+        flags += getattr(P, "FLAGS", {}).get(ps, [])
         for old, new in P.PATCHES[ps]:
             assert s.count(old) == 1, (ps, old[:80], s.count(old))
             s = s.replace(old, new)
@@ -21,7 +23,7 @@ for arg in sys.argv[1:]:
     open(tu, "w").write(s)
     so = os.path.join(R, "exp", "v", name + ".so")
     cmd = ["/opt/rocm/bin/hipcc", "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-           "-I", os.path.join(R, "include"), "-I", os.path.join(R, "minion-plasmid-consensus_amd", "csrc"), "-o", so, tu]
+           "-I", os.path.join(R, "include"), "-I", os.path.join(R, "minion-plasmid-consensus_amd", "csrc"), "-o", so, tu] + flags
     procs.append((name, subprocess.Popen(cmd)))
 for name, p in procs:
     print(name, "ok" if p.wait() == 0 else "FAILED")

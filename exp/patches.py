@@ -239,3 +239,37 @@ PATCHES["p_noscan"] = [("const int ainc = wave_scan_i32(advu);", "const int ainc
                        ("const int aex_rs = wave_scan_max_i32(is_rs ? aex : 0);", "const int aex_rs = is_rs ? aex : 0;")]
 PATCHES["p_nomax"] = [("const int aex_rs = wave_scan_max_i32(is_rs ? aex : 0);", "const int aex_rs = is_rs ? aex : 0;")]
 PATCHES['two'] = [('    // ---- rounds: one token per lane ----\n    int32_t G = 0;  // advances of the window\'s earlier rounds\n    int qc = 0;     // read starts of the window\'s earlier rounds\n    for (int t0 = 0; t0 < T; t0 += 64) {\n      const int t = t0 + l;\n      const bool v = t < T;\n      const uint32_t t0r = W.tok[t], t1r = W.tok[t + 1];  // in bounds for every lane (+64 padding)\n      const uint32_t e0 = v ? t0r : 0u, e1 = v ? t1r : 0u;\n      const int s0 = (int)(e0 & 0xfffu);         // unit start\n      const int pl = (int)((e0 >> 12) & 7u);     // \':\' operand length of a unit\'s prefix (0: none)\n      const int sx = pl ? s0 + pl + 1 : s0;      // the unit\'s main token\n      const bool lfar = v && ((e1 & 0x7fffu) == kFar);\n      const int64_t ex64 = lfar ? C - A : (int64_t)(e1 & 0xfffu);  // far: the token ends at C (beyond the window)\n      const int ex = (int)(ex64 - sx - 1 < kAdvCap ? ex64 : sx + 1 + kAdvCap);\n      const bool is_rs = v && (e0 >> 15);\n      const bool last = v && (e1 >> 15);\n      const uint64_t brs = ballot(is_rs);\n      const int q = qc + lanes_below(brs) + (is_rs ? 1 : 0);\n      // the read\'s slot, loaded before the decode (a read starting in this\n      // round needs no s_val: see the coordinates below)\n      const int32_t q_val = W.s_val[q], q_ts = W.s_ts[q], q_read = W.s_read[q], q_iend = W.s_iend[q];\n      // fast decode from the staged bytes: op, then 4 operand bytes\n      const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage);\n      const int a4 = sx >> 2;\n      const uint32_t sh = (uint32_t)(sx & 3);\n      const uint32_t d0 = b32[a4], d1 = b32[a4 + 1], d2 = b32[a4 + 2];\n      const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, sh);\n      const uint32_t x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);\n      const uint32_t op = x0 & 0xffu;\n      const uint32_t w0 = __builtin_amdgcn_alignbyte(x1, x0, 1u);\n      const int olen = ex - sx - 1;\n      // branch-free decode: op class, 4 operand bytes at once (SWAR)\n      const bool colon = op == \':\', star = op == \'*\', plus = op == \'+\', minus = op == \'-\';\n      const bool spec = colon | star | plus | minus | (op == \'Z\');\n      const bool act = v & spec & ((olen > 0) | last);  // empty operand: skipped unless last (:309, :320)\n      const int ol4 = olen < 0 ? 0 : (olen > 4 ? 4 : olen);\n      const uint32_t vm = ol4 == 4 ? 0xffffffffu : ((1u << (8 * ol4)) - 1u);  // operand bytes in w0\n      //   the unit\'s \':\' operand -- its prefix (pl bytes after s0) or the main\n      //   token\'s own operand -- up to 4 digits: right-align, SWAR decimal\n      const bool pre = pl != 0;\n      const int pa = (s0 + 1) >> 2;\n      const uint32_t pw = __builtin_amdgcn_alignbyte(b32[pa + 1], b32[pa], (uint32_t)((s0 + 1) & 3));\n      const int cl = pre ? pl : (colon ? ol4 : 0);\n      const uint32_t cw = pre ? pw : w0;\n      const uint32_t cvm = cl == 4 ? 0xffffffffu : ((1u << (8 * cl)) - 1u);\n      const uint32_t Tx = cw ^ 0x30303030u;\n      const bool cdig = ((((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u & cvm) == 0;\n      uint32_t X = cl == 0 ? 0u : (Tx & cvm & 0x0F0F0F0Fu) << (8 * (4 - cl));\n      X = mul2561(X) >> 8;\n      X = ((X & 0x00FF00FFu) * 6553601u) >> 16;\n      const int adv_c = (int)(X & 0xffffu);\n      int adv0 = pre ? adv_c : 0;\n      const bool dig_ok = (olen >= 1) & (olen <= 4) & cdig;  // main \':\' token\n      //   bases: (c|0x20) must equal "acgt"[h] with h = (lc>>1)&3 (v_perm table lookup)\n      const uint32_t lc = w0 | 0x20202020u;\n      const uint32_t hh = (lc >> 1) & 0x03030303u;\n      const uint32_t bad = lc ^ __builtin_amdgcn_perm(0u, 0x67746361u, hh);\n      const uint32_t codes = ((hh & 0x01010101u) << 1) | ((hh >> 1) & 0x01010101u);  // dict order A0 T1 C2 G3\n      const int shl = 8 * ((olen - 1) & 3);\n      const bool last_ok = ((bad >> shl) & 0xffu) == 0;  // \'*\': written base = operand[-1] (:96)\n      uint32_t pk = codes;\n      pk = (pk | (pk >> 6)) & 0x000f000fu;\n      pk = (pk | (pk >> 12)) & 0xffu;\n      const uint32_t mstar = 0u - (uint32_t)star;\n      uint32_t pay = (mstar & ((codes >> shl) & 3u)) | (~mstar & (pk & ((1u << (2 * ol4)) - 1u)));\n      const bool slow = lfar | (pre & !cdig) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));\n      const int kop = ((int)star << 1) | ((int)plus * 3) | ((int)minus << 2);  // exclusive classes\n      const int mcol = -(int)colon;\n      int kind = (-(int)act) & ((mcol & (int)(adv_c > 0)) | (~mcol & (-(int)(olen > 0) & kop)));\n      int adv = (-(int)(kind == 1) & adv_c) | (int)(kind == 2) | (-(int)(kind == 4) & (olen < kAdvCap ? olen : kAdvCap));\n      uint32_t err = (v & !spec) ? DE_OP : 0u;  // cs does not start with an operator (:100-102)\n      if (act & star & (olen == 0)) err |= DE_INDEX;  // operand[-1] of \'\' (:96)\n      if ((kind == 2) & !last_ok) err |= DE_KEY;\n      if ((kind == 3) & ((bad & vm) != 0)) err |= DE_KEY;\n      int olen_e = olen;\n      if (slow) {  // rare: decode from HBM\n        const int64_t s = A + sx, e = A + ex64;\n        const TokInfo ti = analyze_long(a.cs, s, e, last);\n        adv = ti.adv; kind = ti.kind; pay = ti.pay; err = ti.err;\n        olen_e = (int)(e - s - 1 < kAdvCap ? e - s - 1 : kAdvCap);\n        if (pl) {\n          const TokInfo tp = analyze_long(a.cs, A + s0, s, false);\n          adv0 = tp.adv;\n          err |= tp.err;\n        }\n      }\n      // ---- coordinates ----\n      const int advu = adv0 + adv;            // unit advance <= 2^21: 64 lanes stay < 2^31\n      const int ainc = wave_scan_i32(advu);\n      const int aex = ainc - advu;\n      const int atot = wave_last_i32(ainc);\n      // a read starting in this round (rs lane j <= l): i = tstart + the\n      // advances since lane j = aex - aex(j); aex never decreases, so aex(j)\n      // is a max-scan over the rs lanes (DPP: no LDS round trip)\n      const int aex_rs = wave_scan_max_i32(is_rs ? aex : 0);\n      if (is_rs) W.s_val[q] = q_ts - (G + aex);  // for later rounds and the window carry\n      const int iu = q > qc ? q_ts + (aex - aex_rs) : q_val + G + aex;  // coordinate at the unit start\n      const int i = iu + adv0;                // ... and at its main token\n      // ---- effects ----\n      uint32_t te = err;\n      if (adv0 > 0 && (iu < 0 || i > n)) te |= DE_INDEX;  // prefix \':\' writes refarr[2 iu + 1 ...] (:75-80)\n      if (kind == 1 && (i < 0 || i + adv > n)) te |= DE_INDEX;\n      if (kind == 2 && (uint32_t)i >= (uint32_t)n) te |= DE_INDEX;\n      if (kind == 3 && (uint32_t)i > (uint32_t)n) te |= DE_INDEX;\n      const int rl = q_read;\n      if (te == 0) {\n        if (kind == 2 && (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);\n        if (kind == 4 && i >= 0 && i < n) {\n          depth_dec(i);\n          depth_inc(i + olen_e < n ? i + olen_e : n);\n        }\n        if (kind == 3) {\n          atomicOr(hl + (i >> 5), 1u << (i & 31));\n          if (olen_e > kInsInline) push_ovf(a, A + sx + 1, rl, i, olen_e);\n        }\n      }\n      if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window\n        const bool sev = te == 0 && kind == 2;\n        const int win = i >> kSubWinBits;\n        for (int ww = 0; ww < a.sub_wins; ++ww) {\n          const uint64_t bw = ballot(sev && win == ww);\n          if (!bw) continue;\n          const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)nsub_v, ww);\n          if (sev && win == ww)\n            a.subev[(int64_t)ww * a.subev_cap + sev_base + n0 + lanes_below(bw)] =\n                (uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay);\n          if (l == ww) nsub_v += (uint32_t)__popcll(bw);\n        }\n      }\n      const bool ins_inline = kind == 3 && olen_e <= kInsInline && te == 0;\n      const uint64_t bins = ballot(ins_inline);\n      if (ins_inline) {\n        a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);\n        atomicAdd(bcnt + i / kBW, 1u);\n      }\n      if (last) {  // the read\'s last operation: i_end, downstream check, span\n        const int ia = i + adv;\n        const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);\n        const int dnf = q_iend & (1 << 30);\n        if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end\n        W.s_iend[q] = ie | dnf;\n        const int ts = q_ts;\n        const int e2 = ie > n ? n : ie;\n        if (ts >= 0 && ts < e2) { depth_inc(ts); depth_dec(e2); }\n      }\n      if (te) flag_read(a, te, rl);\n      G += atot;\n      qc += __popcll(brs);\n      nev += (uint32_t)__popcll(bins);\n    }\n', "    // ---- rounds: two consecutive units per lane (128 per round): the lane's\n    // advances are summed before ONE wave scan, the read-start max-scan keys\n    // on the lane's last start ----\n    int32_t G = 0;  // advances of the window's earlier rounds\n    int qc = 0;     // read starts of the window's earlier rounds\n    struct UnitD { int s0, sx, pl, adv0, adv, kind, olen_e; uint32_t pay, err; bool is_rs, last; };\n    const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage);\n    auto decode = [&](uint32_t e0, uint32_t e1, bool v) {\n      UnitD u;\n      const int s0 = (int)(e0 & 0xfffu);         // unit start\n      const int pl = (int)((e0 >> 12) & 7u);     // ':' operand length of a unit's prefix (0: none)\n      const int sx = pl ? s0 + pl + 1 : s0;      // the unit's main token\n      const bool lfar = v && ((e1 & 0x7fffu) == kFar);\n      const int64_t ex64 = lfar ? C - A : (int64_t)(e1 & 0xfffu);  // far: the token ends at C (beyond the window)\n      const int ex = (int)(ex64 - sx - 1 < kAdvCap ? ex64 : sx + 1 + kAdvCap);\n      const bool last = v && (e1 >> 15);\n      // fast decode from the staged bytes: op, then 4 operand bytes\n      const int a4 = sx >> 2;\n      const uint32_t sh = (uint32_t)(sx & 3);\n      const uint32_t d0 = b32[a4], d1 = b32[a4 + 1], d2 = b32[a4 + 2];\n      const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, sh);\n      const uint32_t x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);\n      const uint32_t op = x0 & 0xffu;\n      const uint32_t w0 = __builtin_amdgcn_alignbyte(x1, x0, 1u);\n      const int olen = ex - sx - 1;\n      const bool colon = op == ':', star = op == '*', plus = op == '+', minus = op == '-';\n      const bool spec = colon | star | plus | minus | (op == 'Z');\n      const bool act = v & spec & ((olen > 0) | last);  // empty operand: skipped unless last (:309, :320)\n      const int ol4 = olen < 0 ? 0 : (olen > 4 ? 4 : olen);\n      const uint32_t vm = ol4 == 4 ? 0xffffffffu : ((1u << (8 * ol4)) - 1u);  // operand bytes in w0\n      const bool pre = pl != 0;\n      const int pa = (s0 + 1) >> 2;\n      const uint32_t pw = __builtin_amdgcn_alignbyte(b32[pa + 1], b32[pa], (uint32_t)((s0 + 1) & 3));\n      const int cl = pre ? pl : (colon ? ol4 : 0);\n      const uint32_t cw = pre ? pw : w0;\n      const uint32_t cvm = cl == 4 ? 0xffffffffu : ((1u << (8 * cl)) - 1u);\n      const uint32_t Tx = cw ^ 0x30303030u;\n      const bool cdig = ((((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u & cvm) == 0;\n      uint32_t X = cl == 0 ? 0u : (Tx & cvm & 0x0F0F0F0Fu) << (8 * (4 - cl));\n      X = mul2561(X) >> 8;\n      X = ((X & 0x00FF00FFu) * 6553601u) >> 16;\n      const int adv_c = (int)(X & 0xffffu);\n      int adv0 = pre ? adv_c : 0;\n      const bool dig_ok = (olen >= 1) & (olen <= 4) & cdig;  // main ':' token\n      const uint32_t lc = w0 | 0x20202020u;\n      const uint32_t hh = (lc >> 1) & 0x03030303u;\n      const uint32_t bad = lc ^ __builtin_amdgcn_perm(0u, 0x67746361u, hh);\n      const uint32_t codes = ((hh & 0x01010101u) << 1) | ((hh >> 1) & 0x01010101u);  // dict order A0 T1 C2 G3\n      const int shl = 8 * ((olen - 1) & 3);\n      const bool last_ok = ((bad >> shl) & 0xffu) == 0;  // '*': written base = operand[-1] (:96)\n      uint32_t pk = codes;\n      pk = (pk | (pk >> 6)) & 0x000f000fu;\n      pk = (pk | (pk >> 12)) & 0xffu;\n      const uint32_t mstar = 0u - (uint32_t)star;\n      uint32_t pay = (mstar & ((codes >> shl) & 3u)) | (~mstar & (pk & ((1u << (2 * ol4)) - 1u)));\n      const bool slow = lfar | (pre & !cdig) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));\n      const int kop = ((int)star << 1) | ((int)plus * 3) | ((int)minus << 2);  // exclusive classes\n      const int mcol = -(int)colon;\n      int kind = (-(int)act) & ((mcol & (int)(adv_c > 0)) | (~mcol & (-(int)(olen > 0) & kop)));\n      int adv = (-(int)(kind == 1) & adv_c) | (int)(kind == 2) | (-(int)(kind == 4) & (olen < kAdvCap ? olen : kAdvCap));\n      uint32_t err = (v & !spec) ? DE_OP : 0u;  // cs does not start with an operator (:100-102)\n      if (act & star & (olen == 0)) err |= DE_INDEX;  // operand[-1] of '' (:96)\n      if ((kind == 2) & !last_ok) err |= DE_KEY;\n      if ((kind == 3) & ((bad & vm) != 0)) err |= DE_KEY;\n      int olen_e = olen;\n      if (slow) {  // rare: decode from HBM\n        const int64_t s = A + sx, e = A + ex64;\n        const TokInfo ti = analyze_long(a.cs, s, e, last);\n        adv = ti.adv; kind = ti.kind; pay = ti.pay; err = ti.err;\n        olen_e = (int)(e - s - 1 < kAdvCap ? e - s - 1 : kAdvCap);\n        if (pl) {\n          const TokInfo tp = analyze_long(a.cs, A + s0, s, false);\n          adv0 = tp.adv;\n          err |= tp.err;\n        }\n      }\n      u.s0 = s0; u.sx = sx; u.pl = pl; u.adv0 = adv0; u.adv = adv; u.kind = kind; u.olen_e = olen_e;\n      u.pay = pay; u.err = err; u.is_rs = v && (e0 >> 15); u.last = last;\n      return u;\n    };\n    // effects of one unit at coordinate iu (unit start); wave-uniform call\n    auto effects = [&](const UnitD& u, int iu, int q, int32_t q_ts, int32_t q_read, int32_t q_iend) {\n      const int adv0 = u.adv0, adv = u.adv, kind = u.kind, olen_e = u.olen_e;\n      const uint32_t pay = u.pay;\n      const int i = iu + adv0;                // coordinate at the main token\n      uint32_t te = u.err;\n      if (adv0 > 0 && (iu < 0 || i > n)) te |= DE_INDEX;  // prefix ':' writes refarr[2 iu + 1 ...] (:75-80)\n      if (kind == 1 && (i < 0 || i + adv > n)) te |= DE_INDEX;\n      if (kind == 2 && (uint32_t)i >= (uint32_t)n) te |= DE_INDEX;\n      if (kind == 3 && (uint32_t)i > (uint32_t)n) te |= DE_INDEX;\n      const int rl = q_read;\n      if (te == 0) {\n        if (kind == 2 && (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);\n        if (kind == 4 && i >= 0 && i < n) {\n          depth_dec(i);\n          depth_inc(i + olen_e < n ? i + olen_e : n);\n        }\n        if (kind == 3) {\n          atomicOr(hl + (i >> 5), 1u << (i & 31));\n          if (olen_e > kInsInline) push_ovf(a, A + u.sx + 1, rl, i, olen_e);\n        }\n      }\n      if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window\n        const bool sev = te == 0 && kind == 2;\n        const int win = i >> kSubWinBits;\n        for (int ww = 0; ww < a.sub_wins; ++ww) {\n          const uint64_t bw = ballot(sev && win == ww);\n          if (!bw) continue;\n          const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)nsub_v, ww);\n          if (sev && win == ww)\n            a.subev[(int64_t)ww * a.subev_cap + sev_base + n0 + lanes_below(bw)] =\n                (uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay);\n          if (l == ww) nsub_v += (uint32_t)__popcll(bw);\n        }\n      }\n      const bool ins_inline = kind == 3 && olen_e <= kInsInline && te == 0;\n      const uint64_t bins = ballot(ins_inline);\n      if (ins_inline) {\n        a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);\n        atomicAdd(bcnt + i / kBW, 1u);\n      }\n      if (u.last) {  // the read's last operation: i_end, downstream check, span\n        const int ia = i + adv;\n        const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);\n        const int dnf = q_iend & (1 << 30);\n        if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end\n        W.s_iend[q] = ie | dnf;\n        const int ts = q_ts;\n        const int e2 = ie > n ? n : ie;\n        if (ts >= 0 && ts < e2) { depth_inc(ts); depth_dec(e2); }\n      }\n      if (te) flag_read(a, te, rl);\n      nev += (uint32_t)__popcll(bins);\n    };\n    constexpr int kTokEnd = tok_cap<WIN>() + 2 + 64 - 1;  // last readable entry\n    for (int t0 = 0; t0 < T; t0 += 128) {\n      const int tA = t0 + 2 * l;\n      const bool vA = tA < T, vB = tA + 1 < T;\n      const uint32_t r0 = W.tok[min(tA, kTokEnd)], r1 = W.tok[min(tA + 1, kTokEnd)], r2 = W.tok[min(tA + 2, kTokEnd)];\n      const uint32_t eA0 = vA ? r0 : 0u, eA1 = vA ? r1 : 0u, eB0 = vB ? r1 : 0u, eB1 = vB ? r2 : 0u;\n      const bool rsA = vA && (eA0 >> 15), rsB = vB && (eB0 >> 15);\n      const uint64_t bA = ballot(rsA), bB = ballot(rsB);\n      const int qA = qc + lanes_below(bA) + lanes_below(bB) + (rsA ? 1 : 0);\n      const int qB = qA + (rsB ? 1 : 0);\n      // the reads' slots, loaded before the decode\n      const int32_t vA_val = W.s_val[qA], vA_ts = W.s_ts[qA], vA_read = W.s_read[qA], vA_iend = W.s_iend[qA];\n      const int32_t vB_val = W.s_val[qB], vB_ts = W.s_ts[qB], vB_read = W.s_read[qB], vB_iend = W.s_iend[qB];\n      const UnitD uA = decode(eA0, eA1, vA);\n      const UnitD uB = decode(eB0, eB1, vB);\n      // ---- coordinates ----\n      const int advA = uA.adv0 + uA.adv, advB = uB.adv0 + uB.adv;  // each <= 2^21: 128 units stay < 2^31\n      const int sum2 = advA + advB;\n      const int ainc = wave_scan_i32(sum2);\n      const int aexA = ainc - sum2, aexB = aexA + advA;  // advances of the round before each unit\n      const int atot = wave_last_i32(ainc);\n      // the latest read start at or before each unit: aex never decreases, so\n      // it is a max-scan of the lanes' last starts (DPP), shifted for unit A\n      const int key = rsB ? aexB : (rsA ? aexA : 0);\n      const int kinc = wave_scan_max_i32(key);\n      const int kprev = (int)from_lane_below((uint32_t)kinc);  // lanes below this one\n      const int krsA = rsA ? aexA : kprev;\n      const int krsB = rsB ? aexB : krsA;\n      if (rsA) W.s_val[qA] = vA_ts - (G + aexA);  // for later rounds and the window carry\n      if (rsB) W.s_val[qB] = vB_ts - (G + aexB);\n      const int iuA = qA > qc ? vA_ts + (aexA - krsA) : vA_val + G + aexA;  // coordinates at the unit starts\n      const int iuB = qB > qc ? vB_ts + (aexB - krsB) : vB_val + G + aexB;\n      effects(uA, iuA, qA, vA_ts, vA_read, vA_iend);\n      effects(uB, iuB, qB, vB_ts, vB_read, vB_iend);\n      G += atot;\n      qc += __popcll(bA) + __popcll(bB);\n    }\n")]
+PATCHES["fl_store"] = [("""        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
+        else atomicAdd(a.rows + row * 4 + code, 1u);
+      }""", """        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
+        else a.rows[row * 4 + code] = 1u;
+      }""")]
+PATCHES["fl_lds2"] = [("""        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
+        else atomicAdd(a.rows + row * 4 + code, 1u);
+      }""", """        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
+        else atomicAdd(wn + ((uint32_t)row & 255u) * 5 + code, 1u);
+      }""")]
+PATCHES["l_nounits"] = [("""  for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+    for (int k = threadIdx.x; k < kBW * kMs; k += blockDim.x) Ml[k] = 0;""", """  for (int64_t u = blockIdx.x; u < nunits && a.N < 0; u += gridDim.x) {
+    for (int k = threadIdx.x; k < kBW * kMs; k += blockDim.x) Ml[k] = 0;""")]
+PATCHES["l_noflank"] = [("""  for (int64_t r0 = fb * blockDim.x; r0 < a.N; r0 += nthreads) {
+    const int64_t r = r0 + threadIdx.x;""", """  for (int64_t r0 = fb * blockDim.x; r0 < a.N && a.N < 0; r0 += nthreads) {
+    const int64_t r = r0 + threadIdx.x;""")]
+PATCHES["l_noevt"] = [("""#pragma unroll
+    for (int q = 0; q < kEPT; ++q) {
+      const uint32_t ev = evs[q];
+      if (ev == ~0u) continue;""", """#pragma unroll
+    for (int q = 0; q < kEPT; ++q) {
+      const uint32_t ev = evs[q];
+      if (ev == ~0u || a.N > 0) continue;""")]
+PATCHES["ept8"] = [("constexpr int kEPT = 16;", "constexpr int kEPT = 8;")]
+PATCHES["ept12"] = [("constexpr int kEPT = 16;", "constexpr int kEPT = 12;")]
+PATCHES["ept10"] = [("constexpr int kEPT = 16;", "constexpr int kEPT = 10;")]
+PATCHES["ept14"] = [("constexpr int kEPT = 16;", "constexpr int kEPT = 14;")]
+FLAGS = {
+  "s_ilp": ["-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+  "s_iilp": ["-mllvm", "-amdgpu-sched-strategy=iterative-ilp"],
+  "s_mmc": ["-mllvm", "-amdgpu-sched-strategy=max-memory-clause"],
+  "s_minreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
+}
+for _k in FLAGS: PATCHES[_k] = []

@@ -273,3 +273,65 @@ FLAGS = {
   "s_minreg": ["-mllvm", "-amdgpu-sched-strategy=iterative-minreg"],
 }
 for _k in FLAGS: PATCHES[_k] = []
+PATCHES["w5"] = [("__global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {",
+                  "__global__ __launch_bounds__(kMaxPW * 64) __attribute__((amdgpu_waves_per_eu(5))) void K_parse(ParseArgs a) {"),
+                 ("    const int max_waves_cu = 16;  // VGPR budget of K_parse (<= 128 VGPRs -> 4 waves per SIMD)",
+                  "    const int max_waves_cu = 20;  // VGPR budget of K_parse (<= 96 VGPRs -> 5 waves per SIMD)"),
+                 ("      for (int nw : {16, 12, 8}) {", "      for (int nw : {16, 12, 10, 8}) {")]
+PATCHES["w5only"] = [PATCHES["w5"][0]]
+PATCHES["flat"] = [("""      uint32_t te = err;
+      if (adv0 > 0 && (iu < 0 || i > n)) te |= DE_INDEX;  // prefix ':' writes refarr[2 iu + 1 ...] (:75-80)
+      if (kind == 1 && (i < 0 || i + adv > n)) te |= DE_INDEX;
+      if (kind == 2 && (uint32_t)i >= (uint32_t)n) te |= DE_INDEX;
+      if (kind == 3 && (uint32_t)i > (uint32_t)n) te |= DE_INDEX;
+      const int rl = q_read;
+      if (te == 0) {
+        if (kind == 2 && (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
+        if (kind == 4 && i >= 0 && i < n) {
+          depth_dec(i);
+          depth_inc(i + olen_e < n ? i + olen_e : n);
+        }
+        if (kind == 3) {
+          atomicOr(hl + (i >> 5), 1u << (i & 31));
+          if (olen_e > kInsInline) push_ovf(a, A + sx + 1, rl, i, olen_e);
+        }
+      }""", """      // data errors and effects as flat predicates (no nested exec-mask regions)
+      const bool bad_i = ((adv0 > 0) & ((iu < 0) | (i > n))) | ((kind == 1) & ((i < 0) | (i + adv > n))) |
+                         ((kind == 2) & ((uint32_t)i >= (uint32_t)n)) | ((kind == 3) & ((uint32_t)i > (uint32_t)n));
+      uint32_t te = err | (bad_i ? DE_INDEX : 0u);
+      const int rl = q_read;
+      const bool ok = te == 0;
+      if (ok & (kind == 2) & (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
+      const bool del = ok & (kind == 4) & (i >= 0) & (i < n);
+      if (del) {
+        depth_dec(i);
+        depth_inc(i + olen_e < n ? i + olen_e : n);
+      }
+      if (ok & (kind == 3)) atomicOr(hl + (i >> 5), 1u << (i & 31));
+      if (ok & (kind == 3) & (olen_e > kInsInline)) push_ovf(a, A + sx + 1, rl, i, olen_e);""")]
+PATCHES["flat2"] = PATCHES["flat"] + [("""      uint32_t err = (v & !spec) ? DE_OP : 0u;  // cs does not start with an operator (:100-102)
+      if (act & star & (olen == 0)) err |= DE_INDEX;  // operand[-1] of '' (:96)
+      if ((kind == 2) & !last_ok) err |= DE_KEY;
+      if ((kind == 3) & ((bad & vm) != 0)) err |= DE_KEY;""",
+"""      uint32_t err = ((v & !spec) ? DE_OP : 0u) |                        // cs does not start with an operator (:100-102)
+                     ((act & star & (olen == 0)) ? DE_INDEX : 0u) |      // operand[-1] of '' (:96)
+                     ((((kind == 2) & !last_ok) | ((kind == 3) & ((bad & vm) != 0))) ? DE_KEY : 0u);"""),
+("""      if (last) {  // the read's last operation: i_end, downstream check, span
+        const int ia = i + adv;
+        const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
+        const int dnf = q_iend & (1 << 30);
+        if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
+        W.s_iend[q] = ie | dnf;
+        const int ts = q_ts;
+        const int e2 = ie > n ? n : ie;
+        if (ts >= 0 && ts < e2) { depth_inc(ts); depth_dec(e2); }
+      }""", """      {  // the read's last operation: i_end, downstream check, span
+        const int ia = i + adv;
+        const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
+        const int dnf = q_iend & (1 << 30);
+        te |= (last & (dnf != 0) & (ia > n)) ? DE_INDEX : 0u;   // rightIndel(2*i) past the end
+        if (last) W.s_iend[q] = ie | dnf;
+        const int ts = q_ts;
+        const int e2 = ie > n ? n : ie;
+        if (last & (ts >= 0) & (ts < e2)) { depth_inc(ts); depth_dec(e2); }
+      }""")]

@@ -857,23 +857,20 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const int iu = q > qc ? q_ts + (aex - aex_rs) : q_val + G + aex;  // coordinate at the unit start
       const int i = iu + adv0;                // ... and at its main token
       // ---- effects ----
-      uint32_t te = err;
-      if (adv0 > 0 && (iu < 0 || i > n)) te |= DE_INDEX;  // prefix ':' writes refarr[2 iu + 1 ...] (:75-80)
-      if (kind == 1 && (i < 0 || i + adv > n)) te |= DE_INDEX;
-      if (kind == 2 && (uint32_t)i >= (uint32_t)n) te |= DE_INDEX;
-      if (kind == 3 && (uint32_t)i > (uint32_t)n) te |= DE_INDEX;
+      // data errors and effects as flat predicates (no nested exec-mask regions)
+      const bool bad_i = ((adv0 > 0) & ((iu < 0) | (i > n))) | ((kind == 1) & ((i < 0) | (i + adv > n))) |
+                         ((kind == 2) & ((uint32_t)i >= (uint32_t)n)) | ((kind == 3) & ((uint32_t)i > (uint32_t)n));
+      uint32_t te = err | (bad_i ? DE_INDEX : 0u);
       const int rl = q_read;
-      if (te == 0) {
-        if (kind == 2 && (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
-        if (kind == 4 && i >= 0 && i < n) {
-          depth_dec(i);
-          depth_inc(i + olen_e < n ? i + olen_e : n);
-        }
-        if (kind == 3) {
-          atomicOr(hl + (i >> 5), 1u << (i & 31));
-          if (olen_e > kInsInline) push_ovf(a, A + sx + 1, rl, i, olen_e);
-        }
+      const bool ok = te == 0;
+      if (ok & (kind == 2) & (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
+      const bool del = ok & (kind == 4) & (i >= 0) & (i < n);
+      if (del) {
+        depth_dec(i);
+        depth_inc(i + olen_e < n ? i + olen_e : n);
       }
+      if (ok & (kind == 3)) atomicOr(hl + (i >> 5), 1u << (i & 31));
+      if (ok & (kind == 3) & (olen_e > kInsInline)) push_ovf(a, A + sx + 1, rl, i, olen_e);
       if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window
         const bool sev = te == 0 && kind == 2;
         const int win = i >> kSubWinBits;

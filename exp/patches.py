@@ -335,3 +335,30 @@ PATCHES["flat2"] = PATCHES["flat"] + [("""      uint32_t err = (v & !spec) ? DE_
         const int e2 = ie > n ? n : ie;
         if (last & (ts >= 0) & (ts < e2)) { depth_inc(ts); depth_dec(e2); }
       }""")]
+PATCHES["sval"] = [
+("      const int32_t q_val = W.s_val[q], q_ts = W.s_ts[q], q_read = W.s_read[q], q_iend = W.s_iend[q];",
+ "      const int32_t q_ts = W.s_ts[q], q_read = W.s_read[q], q_iend = W.s_iend[q];"),
+("""      const int aex_rs = wave_scan_max_i32(is_rs ? aex : 0);
+      if (is_rs) W.s_val[q] = q_ts - (G + aex);  // for later rounds and the window carry
+      const int iu = q > qc ? q_ts + (aex - aex_rs) : q_val + G + aex;  // coordinate at the unit start""",
+"""      // a read starting in this round writes its base into the slot first;
+      // every lane then reads its read's base back (one LDS round trip instead
+      // of a max-scan): i = base + advances before the unit
+      if (is_rs) W.s_val[q] = q_ts - (G + aex);  // for later rounds and the window carry
+      wave_sync_lds();
+      const int iu = W.s_val[q] + G + aex;  // coordinate at the unit start""")]
+PATCHES["bperm"] = [("""      const int aex_rs = wave_scan_max_i32(is_rs ? aex : 0);""",
+"""      // the latest read-start lane <= this one (ballot bits), its aex by one permute
+      const uint64_t m_rs = brs & (l == 63 ? ~0ull : ((2ull << l) - 1ull));
+      const int j_rs = m_rs ? 63 - __clzll((long long)m_rs) : 0;
+      const int aex_j = __shfl(aex, j_rs, 64);
+      const int aex_rs = m_rs ? aex_j : 0;""")]
+PATCHES["ex32"] = [("""      const int64_t ex64 = lfar ? C - A : (int64_t)(e1 & 0xfffu);  // far: the token ends at C (beyond the window)
+      const int ex = (int)(ex64 - sx - 1 < kAdvCap ? ex64 : sx + 1 + kAdvCap);""",
+"""      // far: the token ends at C (beyond the window); 32-bit here (far_c saturates
+      // at 2^30 > kAdvCap + the window), 64-bit only on the slow path
+      const int ex32 = lfar ? far_c : (int)(e1 & 0xfffu);
+      const int ex = ex32 - sx - 1 < kAdvCap ? ex32 : sx + 1 + kAdvCap;"""),
+("""        const int64_t s = A + sx, e = A + ex64;""", """        const int64_t s = A + sx, e = A + (lfar ? C - A : (int64_t)(e1 & 0xfffu));"""),
+("""    int32_t G = 0;  // advances of the window's earlier rounds""", """    const int far_c = (int)(C - A < (1 << 30) ? C - A : (1 << 30));  // wave-uniform
+    int32_t G = 0;  // advances of the window's earlier rounds""")]

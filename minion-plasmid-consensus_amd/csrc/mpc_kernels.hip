@@ -759,6 +759,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     wave_sync_lds();
 
     // ---- rounds: one token per lane ----
+    const int far_c = (int)(C - A < (1 << 30) ? C - A : (1 << 30));  // wave-uniform
     int32_t G = 0;  // advances of the window's earlier rounds
     int qc = 0;     // read starts of the window's earlier rounds
     for (int t0 = 0; t0 < T; t0 += 64) {
@@ -770,15 +771,17 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const int pl = (int)((e0 >> 12) & 7u);     // ':' operand length of a unit's prefix (0: none)
       const int sx = pl ? s0 + pl + 1 : s0;      // the unit's main token
       const bool lfar = v && ((e1 & 0x7fffu) == kFar);
-      const int64_t ex64 = lfar ? C - A : (int64_t)(e1 & 0xfffu);  // far: the token ends at C (beyond the window)
-      const int ex = (int)(ex64 - sx - 1 < kAdvCap ? ex64 : sx + 1 + kAdvCap);
+      // far: the token ends at C (beyond the window); 32-bit here (far_c saturates
+      // at 2^30 > kAdvCap + the window), 64-bit only on the slow path
+      const int ex32 = lfar ? far_c : (int)(e1 & 0xfffu);
+      const int ex = ex32 - sx - 1 < kAdvCap ? ex32 : sx + 1 + kAdvCap;
       const bool is_rs = v && (e0 >> 15);
       const bool last = v && (e1 >> 15);
       const uint64_t brs = ballot(is_rs);
       const int q = qc + lanes_below(brs) + (is_rs ? 1 : 0);
-      // the read's slot, loaded before the decode (a read starting in this
-      // round needs no s_val: see the coordinates below)
-      const int32_t q_val = W.s_val[q], q_ts = W.s_ts[q], q_read = W.s_read[q], q_iend = W.s_iend[q];
+      // the read's slot (tstart, read, i_end), loaded before the decode; its
+      // base s_val is read after this round's read starts have written theirs
+      const int32_t q_ts = W.s_ts[q], q_read = W.s_read[q], q_iend = W.s_iend[q];
       // fast decode from the staged bytes: op, then 4 operand bytes
       const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage);
       const int a4 = sx >> 2;
@@ -834,7 +837,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if ((kind == 3) & ((bad & vm) != 0)) err |= DE_KEY;
       int olen_e = olen;
       if (slow) {  // rare: decode from HBM
-        const int64_t s = A + sx, e = A + ex64;
+        const int64_t s = A + sx, e = A + (lfar ? C - A : (int64_t)(e1 & 0xfffu));
         const TokInfo ti = analyze_long(a.cs, s, e, last);
         adv = ti.adv; kind = ti.kind; pay = ti.pay; err = ti.err;
         olen_e = (int)(e - s - 1 < kAdvCap ? e - s - 1 : kAdvCap);
@@ -849,12 +852,13 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const int ainc = wave_scan_i32(advu);
       const int aex = ainc - advu;
       const int atot = wave_last_i32(ainc);
-      // a read starting in this round (rs lane j <= l): i = tstart + the
-      // advances since lane j = aex - aex(j); aex never decreases, so aex(j)
-      // is a max-scan over the rs lanes (DPP: no LDS round trip)
-      const int aex_rs = wave_scan_max_i32(is_rs ? aex : 0);
+      // a read starting in this round writes its base (tstart - advances before
+      // it) into its slot; every lane then reads its read's base back (one LDS
+      // round trip: fewer instructions than a DPP max-scan over the start
+      // lanes, and the parse is issue-bound): i = base + advances before the unit
       if (is_rs) W.s_val[q] = q_ts - (G + aex);  // for later rounds and the window carry
-      const int iu = q > qc ? q_ts + (aex - aex_rs) : q_val + G + aex;  // coordinate at the unit start
+      wave_sync_lds();
+      const int iu = W.s_val[q] + G + aex;  // coordinate at the unit start
       const int i = iu + adv0;                // ... and at its main token
       // ---- effects ----
       // data errors and effects as flat predicates (no nested exec-mask regions)

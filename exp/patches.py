@@ -362,3 +362,29 @@ PATCHES["ex32"] = [("""      const int64_t ex64 = lfar ? C - A : (int64_t)(e1 & 
 ("""        const int64_t s = A + sx, e = A + ex64;""", """        const int64_t s = A + sx, e = A + (lfar ? C - A : (int64_t)(e1 & 0xfffu));"""),
 ("""    int32_t G = 0;  // advances of the window's earlier rounds""", """    const int far_c = (int)(C - A < (1 << 30) ? C - A : (1 << 30));  // wave-uniform
     int32_t G = 0;  // advances of the window's earlier rounds""")]
+PATCHES["capskip"] = [("""      const int cb = __popc(m);
+      const int inc = wave_scan_i32(cb);
+      if (wave_last_i32(inc) > tok_cap<WIN>()) {""", """      const int cb = __popc(m);
+      // at most tok_cap / 64 boundaries in every lane: no cut (the usual case, no scan)
+      const bool may = ballot(cb > tok_cap<WIN>() / 64) != 0;
+      const int inc = may ? wave_scan_i32(cb) : 0;
+      if (may && wave_last_i32(inc) > tok_cap<WIN>()) {""")]
+PATCHES["subptr"] = [("""        const int win = i >> kSubWinBits;
+        for (int ww = 0; ww < a.sub_wins; ++ww) {
+          const uint64_t bw = ballot(sev && win == ww);
+          if (!bw) continue;
+          const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)nsub_v, ww);
+          if (sev && win == ww)
+            a.subev[(int64_t)ww * a.subev_cap + sev_base + n0 + lanes_below(bw)] =
+                (uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay);
+          if (l == ww) nsub_v += (uint32_t)__popcll(bw);
+        }""", """        const int win = i >> kSubWinBits;
+        uint16_t* wp = a.subev + sev_base;  // window ww's region of this wave
+        for (int ww = 0; ww < a.sub_wins; ++ww, wp += a.subev_cap) {
+          const bool mine = sev && win == ww;
+          const uint64_t bw = ballot(mine);
+          if (!bw) continue;
+          const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)nsub_v, ww);
+          if (mine) wp[n0 + lanes_below(bw)] = (uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay);
+          if (l == ww) nsub_v += (uint32_t)__popcll(bw);
+        }""")]

@@ -675,8 +675,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       hi = hi < 0 ? 0 : (hi > CH ? CH : hi);
       const uint32_t m = em_own & lowmask(hi) & ~lowmask(lo);
       const int cb = __popc(m);
-      const int inc = wave_scan_i32(cb);
-      if (wave_last_i32(inc) > tok_cap<WIN>()) {
+      // at most tok_cap / 64 boundaries in every lane: no cut (the usual case, no scan)
+      const bool may = ballot(cb > tok_cap<WIN>() / 64) != 0;
+      const int inc = may ? wave_scan_i32(cb) : 0;
+      if (may && wave_last_i32(inc) > tok_cap<WIN>()) {
         const int f = __ffsll((unsigned long long)ballot(inc > tok_cap<WIN>())) - 1;
         uint32_t mf = (uint32_t)__builtin_amdgcn_readlane((int)m, f);
         const int j = tok_cap<WIN>() - (__builtin_amdgcn_readlane(inc, f) - __builtin_amdgcn_readlane(cb, f));
@@ -878,13 +880,13 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window
         const bool sev = te == 0 && kind == 2;
         const int win = i >> kSubWinBits;
-        for (int ww = 0; ww < a.sub_wins; ++ww) {
-          const uint64_t bw = ballot(sev && win == ww);
+        uint16_t* wp = a.subev + sev_base;  // window ww's region of this wave
+        for (int ww = 0; ww < a.sub_wins; ++ww, wp += a.subev_cap) {
+          const bool mine = sev && win == ww;
+          const uint64_t bw = ballot(mine);
           if (!bw) continue;
           const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)nsub_v, ww);
-          if (sev && win == ww)
-            a.subev[(int64_t)ww * a.subev_cap + sev_base + n0 + lanes_below(bw)] =
-                (uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay);
+          if (mine) wp[n0 + lanes_below(bw)] = (uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay);
           if (l == ww) nsub_v += (uint32_t)__popcll(bw);
         }
       }

@@ -388,3 +388,11 @@ PATCHES["subptr"] = [("""        const int win = i >> kSubWinBits;
           if (mine) wp[n0 + lanes_below(bw)] = (uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay);
           if (l == ww) nsub_v += (uint32_t)__popcll(bw);
         }""")]
+PATCHES["micro1"] = [("""      const int ex32 = lfar ? far_c : (int)(e1 & 0xfffu);
+      const int ex = ex32 - sx - 1 < kAdvCap ? ex32 : sx + 1 + kAdvCap;""",
+"""      const int ex = lfar ? (far_c - sx - 1 < kAdvCap ? far_c : sx + 1 + kAdvCap) : (int)(e1 & 0xfffu);"""),
+("""        a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);""",
+ """        evp[nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);"""),
+("""  uint32_t nev = 0;                                       // events written (wave-uniform)""",
+ """  uint32_t nev = 0;                                       // events written (wave-uniform)
+  uint64_t* const evp = a.ins_raw + ev_base;""")]

@@ -396,3 +396,31 @@ PATCHES["micro1"] = [("""      const int ex32 = lfar ? far_c : (int)(e1 & 0xfffu
 ("""  uint32_t nev = 0;                                       // events written (wave-uniform)""",
  """  uint32_t nev = 0;                                       // events written (wave-uniform)
   uint64_t* const evp = a.ins_raw + ev_base;""")]
+PATCHES["l32"] = [("""      const int64_t rg = a.read_offset + s_r0[jsq[q]] + (ev >> 16);""",
+"""      const int32_t rg = (int32_t)a.read_offset + s_r0[jsq[q]] + (int32_t)(ev >> 16);  // global reads < 2^30"""),
+("""      if (lb > la) k += vl ? lower_bound_i32(s_vals, la - v0, lb - v0, (int32_t)rg) - (la - v0)
+                           : lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la;""",
+"""      if (lb > la) {
+        if (vl) {  // 32-bit search of the staged RIGHT reads
+          int lo = la - v0, hi = lb - v0;
+          const int l0 = lo;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_vals[mid] < rg) lo = mid + 1; else hi = mid;
+          }
+          k += lo - l0;
+        } else {
+          k += lower_bound_i32(a.vals_out, la, lb, rg) - la;
+        }
+      }""")]
+PATCHES["l32b"] = PATCHES["l32"] + [("""      int64_t k = s_roff[p];
+      if (lb > la) {""", """      int32_t k = s_roff[p];  // run of the event within its gap
+      if (lb > la) {"""),
+("""        atomicMax(a.M + s_rs[p] + g + k, L);
+        uint32_t* rt = a.runt + (s_rs[p] + g + k) * 16;""", """        atomicMax(a.M + s_rs[p] + g + (int64_t)k, L);
+        uint32_t* rt = a.runt + (s_rs[p] + g + (int64_t)k) * 16;""")]
+PATCHES["l4"] = PATCHES["l32b"] + [("""        for (int j = 0; j < L; ++j) atomicAdd(tp + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
+      } else {""", """#pragma unroll
+        for (int j = 0; j < kInsInline; ++j)  // straight-line: bases j < L
+          if (j < L) atomicAdd(tp + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
+      } else {""")]

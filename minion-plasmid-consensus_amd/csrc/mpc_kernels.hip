@@ -1562,22 +1562,35 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       if (ev == ~0u) continue;
       const int gap = g0 + (int)((ev >> 10) & (kBW - 1));
       const int64_t g = (int64_t)gb + gap;
-      const int64_t rg = a.read_offset + s_r0[jsq[q]] + (ev >> 16);
+      const int32_t rg = (int32_t)a.read_offset + s_r0[jsq[q]] + (int32_t)(ev >> 16);  // global reads < 2^30
       const int L = (int)((ev >> 8) & 3u) + 1;
       const int p = gap - g0;
       const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
-      int64_t k = s_roff[p];
-      if (lb > la) k += vl ? lower_bound_i32(s_vals, la - v0, lb - v0, (int32_t)rg) - (la - v0)
-                           : lower_bound_i32(a.vals_out, la, lb, (int32_t)rg) - la;
+      int32_t k = s_roff[p];  // run of the event within its gap
+      if (lb > la) {
+        if (vl) {  // 32-bit search of the staged RIGHT reads
+          int lo = la - v0, hi = lb - v0;
+          const int l0 = lo;
+          while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (s_vals[mid] < rg) lo = mid + 1; else hi = mid;
+          }
+          k += lo - l0;
+        } else {
+          k += lower_bound_i32(a.vals_out, la, lb, rg) - la;
+        }
+      }
       // the bases too, run-relative (LEFT: base bi from the 3' end lands on the
       // run's slot hi_run - 1 - bi, :37-62): K_ins maps them to rows after the layout
       if (k < kKMax) {
         atomicMax(&Ml[p * kMs + k], (uint32_t)L);
         uint32_t* tp = Tl + p * kTs + k * 16;
-        for (int j = 0; j < L; ++j) atomicAdd(tp + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
+#pragma unroll
+        for (int j = 0; j < kInsInline; ++j)  // straight-line: bases j < L
+          if (j < L) atomicAdd(tp + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
       } else {
-        atomicMax(a.M + s_rs[p] + g + k, L);
-        uint32_t* rt = a.runt + (s_rs[p] + g + k) * 16;
+        atomicMax(a.M + s_rs[p] + g + (int64_t)k, L);
+        uint32_t* rt = a.runt + (s_rs[p] + g + (int64_t)k) * 16;
         for (int j = 0; j < L; ++j) atomicAdd(rt + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
       }
     }

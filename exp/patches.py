@@ -424,3 +424,49 @@ PATCHES["l4"] = PATCHES["l32b"] + [("""        for (int j = 0; j < L; ++j) atomi
         for (int j = 0; j < kInsInline; ++j)  // straight-line: bases j < L
           if (j < L) atomicAdd(tp + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
       } else {""")]
+PATCHES["f32"] = [("""      for (int x = tid; x < cn; x += blockDim.x) {
+        const uint32_t word = bm[x >> 5];
+        const int o = wpre[x >> 5] + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
+        const int32_t rw = t_row[o];
+        if (rw < 0) continue;
+        const int64_t row = (int64_t)rw + (c0 + x - t_start[o]);
+        const int code = code_exact(stage[x + sh0]);
+        if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
+        const int64_t wr = row - w0;
+        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
+        else atomicAdd(a.rows + row * 4 + code, 1u);
+      }""", """      // 32-bit: rows < row_cap < 2^31, a block's flank bytes < 2^31
+      const int cn32 = (int)cn, c032 = (int)c0;
+      const int32_t w032 = w0 >= 0 ? (int32_t)w0 : -(1 << 30);  // no window: never a hit
+      for (int x = tid; x < cn32; x += blockDim.x) {
+        const uint32_t word = bm[x >> 5];
+        const int o = wpre[x >> 5] + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
+        const int32_t rw = t_row[o];
+        if (rw < 0) continue;
+        const int32_t row = rw + (c032 + x - t_start[o]);
+        const int code = code_exact(stage[x + sh0]);
+        if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
+        const uint32_t wr = (uint32_t)(row - w032);
+        if (wr < (uint32_t)kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
+        else atomicAdd(a.rows + (int64_t)row * 4 + code, 1u);
+      }""")]
+PATCHES["epi32"] = [("""  return ((uint32_t)raw & 0x3ffu) | ((gap % (uint32_t)kBW) << 10) | ((uint32_t)((int64_t)(raw >> 32) - rg0) << 16);""",
+"""  return ((uint32_t)raw & 0x3ffu) | ((gap % (uint32_t)kBW) << 10) | (((uint32_t)(raw >> 32) - (uint32_t)rg0) << 16);""")]
+PATCHES["i32"] = [("""    const int64_t t0 = (int64_t)a.right_start[g] + g, t1 = (int64_t)a.right_start[g + 1] + g + 1;
+    const int64_t top = (int64_t)a.row_base[g] + a.lo_f[g] - 1;
+    const bool excl = no_ovf && t1 - t0 == 1;
+    for (int64_t t = t0; t < t1; ++t) {
+      uint4* rt = reinterpret_cast<uint4*>(a.runt + t * 16);""", """    // 32-bit: runs < n_reads_global + gaps < 2^31, rows < 2^31
+    const int32_t gi = (int32_t)g;
+    const int32_t t0 = a.right_start[g] + gi, t1 = a.right_start[g + 1] + gi + 1;
+    const int32_t top = a.row_base[g] + a.lo_f[g] - 1;
+    const bool excl = no_ovf && t1 - t0 == 1;
+    for (int32_t t = t0; t < t1; ++t) {
+      uint4* rt = reinterpret_cast<uint4*>(a.runt) + 4 * (int64_t)t;"""),
+("""      const int64_t rtop = top + a.hiR[t];
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi) {
+        uint32_t* row = a.rows + (rtop - bi) * 4;""", """      const int32_t rtop = top + a.hiR[t];
+#pragma unroll
+      for (int bi = 0; bi < 4; ++bi) {
+        uint32_t* row = a.rows + (int64_t)(rtop - bi) * 4;""")]

@@ -2028,17 +2028,20 @@ __global__ __launch_bounds__(kFR) void K_flank(FlankArgs a) {
       // consecutive lanes take consecutive bytes: a flank's bytes go to
       // consecutive rows, so a wave's (rare) global atomics cover a few
       // contiguous segments instead of one scattered row per lane
-      for (int x = tid; x < cn; x += blockDim.x) {
+      // 32-bit: rows < row_cap < 2^31, a block's flank bytes < 2^31
+      const int cn32 = (int)cn, c032 = (int)c0;
+      const int32_t w032 = w0 >= 0 ? (int32_t)w0 : -(1 << 30);  // no window: never a hit
+      for (int x = tid; x < cn32; x += blockDim.x) {
         const uint32_t word = bm[x >> 5];
         const int o = wpre[x >> 5] + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
         const int32_t rw = t_row[o];
         if (rw < 0) continue;
-        const int64_t row = (int64_t)rw + (c0 + x - t_start[o]);
+        const int32_t row = rw + (c032 + x - t_start[o]);
         const int code = code_exact(stage[x + sh0]);
         if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
-        const int64_t wr = row - w0;
-        if (wr >= 0 && wr < kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
-        else atomicAdd(a.rows + row * 4 + code, 1u);
+        const uint32_t wr = (uint32_t)(row - w032);
+        if (wr < (uint32_t)kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
+        else atomicAdd(a.rows + (int64_t)row * 4 + code, 1u);
       }
     }
   }

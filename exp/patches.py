@@ -470,3 +470,8 @@ PATCHES["i32"] = [("""    const int64_t t0 = (int64_t)a.right_start[g] + g, t1 =
 #pragma unroll
       for (int bi = 0; bi < 4; ++bi) {
         uint32_t* row = a.rows + (int64_t)(rtop - bi) * 4;""")]
+PATCHES["evlocal"] = [
+("""        a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);""",
+ """        a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, rl);"""),
+("""  const int64_t rg0 = a.read_offset + r0;  // the workgroup's first (global) read""",
+ """  const int64_t rg0 = r0;  // the workgroup's first read (raw events hold launch-local reads)""")]

@@ -475,3 +475,32 @@ PATCHES["evlocal"] = [
  """        a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, rl);"""),
 ("""  const int64_t rg0 = a.read_offset + r0;  // the workgroup's first (global) read""",
  """  const int64_t rg0 = r0;  // the workgroup's first read (raw events hold launch-local reads)""")]
+PATCHES["tok2"] = [("""      const uint32_t t0r = W.tok[t], t1r = W.tok[t + 1];  // in bounds for every lane (+64 padding)""",
+"""      // entries t, t + 1 from one ds_read2 of the dwords holding them (in bounds: +64 padding)
+      const uint32_t* tk32 = reinterpret_cast<const uint32_t*>(W.tok);
+      const uint32_t da = tk32[t >> 1], db = tk32[(t >> 1) + 1];
+      const bool odd = (t & 1) != 0;
+      const uint32_t t0r = odd ? (da >> 16) : (da & 0xffffu);
+      const uint32_t t1r = odd ? (db & 0xffffu) : (da >> 16);""")]
+PATCHES["cmp2"] = [("""      uint32_t m = tu;
+      while (m) {
+        const int k = __ffs(m) - 1;
+        m &= m - 1;
+        W.tok[idx++] = (uint16_t)((uint32_t)(base + k) | (((pl0 >> k) & 1u) << 12) | (((pl1 >> k) & 1u) << 13) |
+                                  (((p5 >> k) & 1u) << 14) | (((ra_own >> k) & 1u) << 15));
+      }""", """      uint32_t m = tu;
+      auto entry = [&](int k) {
+        return (uint16_t)((uint32_t)(base + k) | (((pl0 >> k) & 1u) << 12) | (((pl1 >> k) & 1u) << 13) |
+                          (((p5 >> k) & 1u) << 14) | (((ra_own >> k) & 1u) << 15));
+      };
+      while (m) {  // two entries per trip (half the loop control)
+        const int k1 = __ffs(m) - 1;
+        m &= m - 1;
+        W.tok[idx] = entry(k1);
+        if (m) {
+          const int k2 = __ffs(m) - 1;
+          m &= m - 1;
+          W.tok[idx + 1] = entry(k2);
+        }
+        idx += 2;
+      }""")]

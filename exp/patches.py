@@ -504,3 +504,38 @@ PATCHES["cmp2"] = [("""      uint32_t m = tu;
         }
         idx += 2;
       }""")]
+PATCHES["mdepth"] = [("""      const bool del = ok & (kind == 4) & (i >= 0) & (i < n);
+      if (del) {
+        depth_dec(i);
+        depth_inc(i + olen_e < n ? i + olen_e : n);
+      }
+""", ""),
+("""      if (last) {  // the read's last operation: i_end, downstream check, span
+        const int ia = i + adv;
+        const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
+        const int dnf = q_iend & (1 << 30);
+        if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
+        W.s_iend[q] = ie | dnf;
+        const int ts = q_ts;
+        const int e2 = ie > n ? n : ie;
+        if (ts >= 0 && ts < e2) { depth_inc(ts); depth_dec(e2); }
+      }""", """      {  // depth differences: a deletion (-1 at i, +1 at its end) and / or, at the
+         // read's last operation, its span (+1 at tstart, -1 at its end): one
+         // exec region for the usual single update, a second for both
+        const int ia = i + adv;
+        const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
+        const int dnf = q_iend & (1 << 30);
+        const int ts = q_ts;
+        const int e2 = ie > n ? n : ie;
+        const bool del = ok & (kind == 4) & (i >= 0) & (i < n);
+        const bool span = last & (ts >= 0) & (ts < e2);
+        if (del | span) {
+          depth_dec(del ? i : e2);
+          depth_inc(del ? (i + olen_e < n ? i + olen_e : n) : ts);
+        }
+        if (del & span) { depth_inc(ts); depth_dec(e2); }
+        if (last) {  // the read's last operation: i_end, downstream check
+          if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
+          W.s_iend[q] = ie | dnf;
+        }
+      }""")]

@@ -203,7 +203,7 @@ struct Flank {
 
 extern "C" {
 
-int mpc_ingest_version(void) { return 1; }
+int mpc_ingest_version(void) { return 2; }  // 2: + mpc_write_calls, mpc_py_float_repr, pseudopair
 
 void mpc_ingest_free(mpc_ingest_out* o) {
   if (!o) return;

@@ -10,8 +10,11 @@
 //               f64 division then one f64 multiply, printed like Python's
 //               float repr (shortest round-trip digits, fixed notation for
 //               decimal exponents in (-4, 16], else e-notation)          (:431, :460-463)
-// The calls are formatted by all cores in chunks and written in order; outputs
-// are opened only after everything is formatted (no partial files).
+// The calls are formatted by all cores in chunks and written in order.  Only the
+// formatting happens before any file is opened; the three files are then opened
+// and written one after the other, as the reference does (:447, :453, :460), so
+// an open/write failure on a later file leaves the earlier ones written, exactly
+// like the reference (Snakemake removes the outputs of a failed job).
 #include <charconv>
 #include <cmath>
 #include <cstdint>

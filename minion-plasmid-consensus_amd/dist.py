@@ -246,7 +246,16 @@ class ShardedPileup:
         cap = self.ex.max_int([cap] * local)[0] if isinstance(self.ex, DistExchange) else cap
         self.plans = [eng.Plan(b, cap) for b in self.batches]
         self._sized = False
+        # runs in use, read back once: valid for THESE batches only -- the
+        # batches are fixed for the object's lifetime (mpc_plan_set_input is
+        # never called on them); rebind() resets it
         self._used = None
+
+    def rebind(self):
+        """Forget the cached run count (call after changing any shard's inputs
+        in place): the next step re-reads it before the run-array MAX."""
+        self._used = None
+        self._sized = False
 
     # bench.py interface (one local shard)
     @property

@@ -141,6 +141,7 @@ class _IngestOut(ctypes.Structure):
 
 
 INGEST_OK, INGEST_ERROR, INGEST_FALLBACK = 0, 1, 2
+INGEST_ABI = 2  # mpc_ingest_version() of the library these bindings expect
 _ingest_lib = None
 
 
@@ -149,13 +150,17 @@ def _native():
     if _ingest_lib is None:
         from . import _build
         path = _build.LIBINGEST
-        if not os.path.exists(path):
-            try:
-                _build.build_ingest()
-            except Exception:  # no compiler: the Python ingest is used
+        try:
+            _build.build_ingest()  # no-op unless missing or older than its sources
+        except Exception:  # no compiler: a present library is still used, else the Python ingest
+            if not os.path.exists(path):
                 _ingest_lib = False
                 return None
         L = ctypes.CDLL(path)
+        L.mpc_ingest_version.restype = ctypes.c_int
+        if L.mpc_ingest_version() != INGEST_ABI:
+            raise IngestError(f"{path}: ABI {L.mpc_ingest_version()} != {INGEST_ABI} (stale build: "
+                              "rebuild with __graft_entry__.build())")
         L.mpc_ingest.restype = ctypes.c_int
         L.mpc_ingest.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                  ctypes.POINTER(_IngestOut)]

@@ -91,7 +91,11 @@ def main(argv=None):
         statprint("Max depth is {}.".format(res["max_depth"]))
         statprint("DEPTH_THRESHOLD is {}.".format(res["max_depth"] * args.MIN_DEPTH_FACTOR))
         statprint("Writing consensus, chromatogram data and per-position consensus accuracies...")
-        writers.write_outputs(res, c, ch, acc)
+        try:
+            writers.write_outputs(res, c, ch, acc)
+        except OSError as e:  # WriteError included: the reference's open()/write() raise -> exit 1
+            print("Error: {}".format(e), file=sys.stderr)
+            return 1
     for src, dst in args.revcomp:
         statprint("Reverse-complementing {} into {}...".format(src, dst))
         try:

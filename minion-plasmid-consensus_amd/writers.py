@@ -51,8 +51,9 @@ def write_outputs(calls, consensus_path, chromat_path, accuracies_path, n_thread
     import ctypes
     from . import ingest
     L = ingest._native()
-    if L is None:
-        raise WriteError("libmpc_ingest.so (native writers) is not built")
+    if L is None:  # no host compiler to build the native writers: same formats in Python
+        write_outputs_python(calls, consensus_path, chromat_path, accuracies_path)
+        return
     raw = np.ascontiguousarray(calls["raw"], dtype=np.uint32).reshape(-1, 4)
     msg = ctypes.create_string_buffer(256)
     buf = raw if raw.size else np.zeros((1, 4), np.uint32)

@@ -28,8 +28,10 @@ Output: one JSON line (rank 0) with the contract fields plus
                 and under "reference" the reference script itself timed in the
                 build container (profiles/ref_cpu_baseline.json,
                 scripts/time_reference.py)
-  e2e           (N=1, c1/c2/c4) the drop-in CLI on files of the same workload:
-                ingest + H2D + kernels + D2H + writers, wall clock
+  e2e           (N=1, every config) the drop-in CLI on files of the same
+                workload, all of the GPU's jobs in one call (c5: 24 jobs, 72
+                output files): ingest + H2D + kernels + D2H + writers, wall
+                clock, with the phase split
 """
 import argparse
 import contextlib
@@ -66,7 +68,7 @@ CONFIGS = {
 }
 C5_PER_GPU = 12
 PORT_SAMPLE_BASES = 2_500_000_000  # bound of the live CPU-port timing (~6 s of C at ~4e8 b/s)
-E2E_CONFIGS = ("c1", "c2", "c4")
+E2E_CONFIGS = ("c1", "c2", "c3", "c4", "c5")
 
 
 def shard_samples(pkg, cfg, rank, world):
@@ -122,38 +124,52 @@ def reference_record(cfg):
     return r
 
 
-def e2e_cli(pkg, cfg, samples_n, reads, seed, profile, antisense, reps=2):
-    """Wall time of the drop-in CLI (both strands in one launch) on files of this
-    config: ingest + H2D + kernels + D2H + writers.  Returns a dict."""
+def e2e_cli(pkg, cfg, reps=2):
+    """Wall time of the drop-in CLI on files of this config, all of a GPU's jobs
+    in ONE CLI call (c2/c4: --also for the antisense strand; c5: --job per
+    plasmid and strand, 12 plasmids = 24 jobs = 72 output files): native ingest
+    + H2D + plan + kernels + D2H + native writers.  Returns a dict with the
+    phase split (ingest / device / write) of the best repetition."""
     cli = importlib.import_module("minion-plasmid-consensus_amd.mapped_paf_read_parser")
-    n = samples_n
+    n, reads, _, profile, seed, antisense, _ = CONFIGS[cfg]
     tmp = tempfile.mkdtemp(prefix="mpc_e2e_")
     try:
-        syn = pkg.synth.Synth(n=n, n_reads=reads, profile=profile, seed=seed, antisense=antisense)
-        aligned = int(sum(int(syn.sample(s)["aligned"].sum()) for s in range(2 if antisense else 1)))
         p = lambda f: os.path.join(tmp, f)
-        syn.write_files(p("ref.fa"), p("reads.fa"), p("s0.paf"), p("ref1.fa") if antisense else None,
-                        p("s1.paf") if antisense else None)
+        plasmids = C5_PER_GPU if cfg == "c5" else 1
+        argv, aligned, n_files = [], 0, 0
+        for k in range(plasmids):
+            syn = pkg.synth.Synth(n=n, n_reads=reads, profile=profile, seed=seed + k, antisense=antisense)
+            aligned += int(sum(int(syn.sample(s)["aligned"].sum()) for s in range(2 if antisense else 1)))
+            syn.write_files(p(f"ref{k}.fa"), p(f"reads{k}.fa"), p(f"s0_{k}.paf"), p(f"ref{k}_as.fa") if antisense else None,
+                            p(f"s1_{k}.paf") if antisense else None)
+            del syn
+            strands = [(p(f"ref{k}.fa"), p(f"s0_{k}.paf"))] + ([(p(f"ref{k}_as.fa"), p(f"s1_{k}.paf"))] if antisense else [])
+            for s, (ref, paf) in enumerate(strands):
+                argv += ["--job", ref, paf, p(f"reads{k}.fa"), p(f"c{k}_{s}.fa"), p(f"ch{k}_{s}.tsv"), p(f"acc{k}_{s}.tsv")]
+                n_files += 3
+        argv += ["--min_depth_factor", "0.1", "--global_threshold_factor", "5"]
         in_bytes = sum(os.path.getsize(p(f)) for f in os.listdir(tmp))
-        argv = ["--ref", p("ref.fa"), "--reads", p("reads.fa"), "--paf", p("s0.paf"), "--consensus", p("c0.fa"),
-                "--chromat", p("ch0.tsv"), "--accuracies", p("acc0.tsv"), "--min_depth_factor", "0.1",
-                "--global_threshold_factor", "5"]
-        if antisense:
-            argv += ["--also", p("ref1.fa"), p("s1.paf"), p("c1.fa"), p("ch1.tsv"), p("acc1.tsv")]
-        walls = []
+        runs = []
         for _ in range(reps):
             sink = io.StringIO()
+            tm = {}
             t0 = time.perf_counter()
             with contextlib.redirect_stdout(sink):
-                rc = cli.main(argv)
-            walls.append(time.perf_counter() - t0)
+                rc = cli.main(argv, timings=tm)
+            tm["wall"] = time.perf_counter() - t0
+            runs.append(tm)
             if rc != 0:
                 raise RuntimeError(f"CLI exit {rc}")
-        return {"value": aligned / min(walls), "unit": "aligned bases/s", "wall_s": min(walls),
-                "wall_s_first": walls[0], "aligned_bases": aligned, "input_bytes": in_bytes,
-                "what": f"{cfg} files ({'2 strands, --also: one launch' if antisense else '1 strand'}); "
+        best = min(runs, key=lambda r: r["wall"])
+        out_bytes = sum(os.path.getsize(p(f)) for f in os.listdir(tmp) if f.startswith(("c", "acc")) and "_" in f)
+        return {"value": aligned / best["wall"], "unit": "aligned bases/s", "wall_s": best["wall"],
+                "wall_s_first": runs[0]["wall"], "aligned_bases": aligned, "input_bytes": in_bytes,
+                "output_files": n_files, "output_bytes": out_bytes,
+                "phases_s": {k: round(best[k], 4) for k in ("ingest", "device", "write")},
+                "write_frac": best["write"] / best["wall"],
+                "what": f"{cfg} files, {len(argv) // 7} job(s) in ONE CLI call (--job each), {n_files} output files; "
                         "CLI main(): native ingest of ref/PAF/reads FASTA + H2D + plan + kernels + D2H + "
-                        "writers of the three output files; best of %d (first includes allocations)" % reps}
+                        "writers of the output files; best of %d (first includes allocations)" % reps}
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 
@@ -261,7 +277,7 @@ def main():
     if rank == 0 and world == 1 and not args.no_e2e and cfg in E2E_CONFIGS:
         del runner, plan, batch
         torch.cuda.empty_cache()
-        e2e = e2e_cli(pkg, cfg, n, reads, seed, profile, antisense)
+        e2e = e2e_cli(pkg, cfg)
 
     if rank == 0:
         line = {

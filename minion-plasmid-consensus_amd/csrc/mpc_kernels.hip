@@ -153,6 +153,30 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int j) {
   return (int64_t)(((uint64_t)(uint32_t)hi << 32) | (uint32_t)lo);
 }
 
+// Diagnostic build only (-DMPC_STAMPS, scripts/kparse_stamps.py): s_memtime
+// stamps around K_parse's segments, summed per wave in scalar registers and
+// stored once per wave into g_stamps (nothing else reads them).  The product
+// build compiles none of this.
+#ifdef MPC_STAMPS
+constexpr int kStampSeg = 8, kStampWaves = 1 << 16;
+__device__ uint64_t g_stamps[kStampWaves * kStampSeg];
+#define MPC_STAMP(t)                                                                   \
+  do {                                                                               \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");        \
+    __builtin_amdgcn_sched_barrier(0);                                               \
+  } while (0)
+#define MPC_SEG(k)                  \
+  do {                              \
+    uint64_t t_;                    \
+    MPC_STAMP(t_);                  \
+    st_acc[k] += t_ - st_prev;      \
+    st_prev = t_;                   \
+  } while (0)
+#else
+#define MPC_SEG(k) do {} while (0)
+#endif
+
 // ---------------------------------------------------------------------------
 // K_parse: Step 4 of the reference (:285-323 tokenizer, :74-104 processOperation)
 // ---------------------------------------------------------------------------
@@ -553,6 +577,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   int64_t* wbase = reinterpret_cast<int64_t*>(wcnt + kMaxPW);                  // [kMaxPW] event region per wave
   uint32_t* hl = reinterpret_cast<uint32_t*>(wbase + kMaxPW);                  // LEFT gaps bitmap
   const int4 wk = a.work[blockIdx.x];
+#ifdef MPC_STAMPS
+  uint64_t st_acc[kStampSeg] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev;
+  MPC_STAMP(st_prev);
+#endif
   const int smp = wk.x;
   const int64_t r0 = wk.y, r1 = wk.z;
   const int n = a.n_of[smp];
@@ -607,6 +635,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     int64_t E = A + WIN < wend ? A + WIN : wend;
     const int64_t o63 = readlane64(cur.o, 63);
     if (o63 < E) E = o63;
+    MPC_SEG(0);
     const int64_t o_nx = __shfl(cur.o, (l + 1) & 63, 64);
     const uint32_t uo_nx = (uint32_t)__shfl((int)cur.uo, (l + 1) & 63, 64);
     const uint32_t dno_nx = (uint32_t)__shfl((int)cur.dno, (l + 1) & 63, 64);
@@ -759,6 +788,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if (l == 0) W.tok[T] = far ? (uint16_t)(kFar | (c_rs ? 0x8000u : 0u)) : (uint16_t)((C - A) | (c_rs ? 0x8000u : 0u));
     }
     wave_sync_lds();
+    MPC_SEG(1);
 
     // ---- rounds: one token per lane ----
     const int far_c = (int)(C - A < (1 << 30) ? C - A : (1 << 30));  // wave-uniform
@@ -849,6 +879,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
           err |= tp.err;
         }
       }
+      MPC_SEG(2);
       // ---- coordinates ----
       const int advu = adv0 + adv;            // unit advance <= 2^21: 64 lanes stay < 2^31
       const int ainc = wave_scan_i32(advu);
@@ -862,6 +893,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       wave_sync_lds();
       const int iu = W.s_val[q] + G + aex;  // coordinate at the unit start
       const int i = iu + adv0;                // ... and at its main token
+      MPC_SEG(3);
       // ---- effects ----
       // data errors and effects as flat predicates (no nested exec-mask regions)
       const bool bad_i = ((adv0 > 0) & ((iu < 0) | (i > n))) | ((kind == 1) & ((i < 0) | (i + adv > n))) |
@@ -910,6 +942,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       G += atot;
       qc += __popcll(brs);
       nev += (uint32_t)__popcll(bins);
+      MPC_SEG(4);
     }
     wave_sync_lds();
     // ---- reads that ended in this window: i_end; carry the open one ----
@@ -928,6 +961,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     P = Pn;
     rs0 = rsn;
     if (Pn < wend) cur = fetch_window<CH>(a, Pn, rsn, l);
+    MPC_SEG(5);
   }
   // reads starting at the range end have an empty cs
   for (int64_t r = rs0 + l; r < rb; r += 64) {
@@ -937,9 +971,21 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   }
   if (l == 0) { wcnt[w] = nev; wbase[w] = ev_base; }
   if (TM == 3 && l < a.sub_wins) a.subev_cnt[((int64_t)blockIdx.x * kMaxPW + w) * kMaxSubWins + l] = nsub_v;
+  MPC_SEG(5);
   __syncthreads();
+  MPC_SEG(6);
   parse_epilogue<TM>(a, n, gb, nbk, r0, hl, bcnt, uni, wcnt, wbase, nw, reinterpret_cast<uint64_t*>(lds),
                      nw * (int)sizeof(WL) / 8);
+#ifdef MPC_STAMPS
+  MPC_SEG(7);
+  const int64_t gw = (int64_t)blockIdx.x * kMaxPW + w;
+  if (l < kStampSeg && gw < kStampWaves) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < kStampSeg; ++k) v = l == k ? st_acc[k] : v;
+    g_stamps[gw * kStampSeg + l] = v;
+  }
+#endif
 }
 
 
@@ -2913,6 +2959,20 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
+
+#ifdef MPC_STAMPS
+// diagnostic build only: per-wave K_parse segment cycle sums (kStampSeg per wave)
+int mpc_debug_stamps(uint64_t* out, int64_t n_words) {
+  const int64_t nw = std::min<int64_t>(n_words, (int64_t)kStampWaves * kStampSeg);
+  HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)nw * 8, 0, hipMemcpyDeviceToHost));
+  return MPC_OK;
+}
+int mpc_debug_stamps_clear(void) {
+  static std::vector<uint64_t> z((size_t)kStampWaves * kStampSeg, 0);
+  HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(g_stamps), z.data(), z.size() * 8, 0, hipMemcpyHostToDevice));
+  return MPC_OK;
+}
+#endif
 
 int mpc_run(mpc_plan* p, double mdf, double gtf, void* stream) {
   int rc;

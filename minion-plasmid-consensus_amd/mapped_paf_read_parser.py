@@ -12,6 +12,10 @@ Extra, optional flags (defaults keep the reference behaviour):
   --revcomp SRC DST  after writing, reverse-complement consensus SRC into DST
                      (Snakefile rule revcomp_antisense_consensus, :425-450);
                      repeatable
+  --job REF PAF READS CONSENSUS CHROMAT ACCURACIES
+                     another job with its OWN reads file, same launch (a batch of
+                     plasmids: BASELINE configs[4]); repeatable.  With --job the
+                     primary --ref/--paf/--reads/... flags may be omitted.
 """
 import argparse
 import importlib
@@ -54,11 +58,17 @@ def build_parser():
                    help="additional (assembly, PAF) job against the same reads, same launch")
     p.add_argument("--revcomp", nargs=2, action="append", default=[], metavar=("SRC", "DST"),
                    help="reverse-complement a written consensus file (rule revcomp_antisense_consensus)")
+    p.add_argument("--job", nargs=6, action="append", default=[],
+                   metavar=("REF", "PAF", "READS", "CONSENSUS", "CHROMAT", "ACCURACIES"),
+                   help="additional job with its own reads file, same launch")
     return p
 
 
-def main(argv=None):
+def main(argv=None, timings=None):
+    """CLI entry.  ``timings`` (a dict, optional) receives the wall seconds of
+    the phases: ingest, device (H2D + kernels + D2H), write."""
     args = build_parser().parse_args(argv)
+    tm = timings if timings is not None else {}
     pkg = _pkg()
     ingest, engine, writers = pkg.ingest, pkg.engine, pkg.writers
     print("=======================================================")
@@ -70,24 +80,32 @@ def main(argv=None):
     print("Time: {}".format(time.strftime("%Y/%m/%d %T")))
     print("Engine: libmpc (HIP, gfx950)")
     print("=======================================================\n")
-    jobs = [(args.REF, args.PAF, args.consensus, args.chromat, args.accuracies)] + [tuple(a) for a in args.also]
+    # (ref, paf, reads, consensus, chromat, accuracies) per job
+    jobs = [] if (args.job and args.REF is None) else \
+        [(args.REF, args.PAF, args.READS, args.consensus, args.chromat, args.accuracies)]
+    jobs += [(r, p, args.READS, c, ch, a) for r, p, c, ch, a in args.also] + [tuple(j) for j in args.job]
+    t0 = time.perf_counter()
     try:
         samples = []
-        for ref, paf, *_ in jobs:
+        for ref, paf, reads, *_ in jobs:
             statprint(f"Ingesting {paf} against {ref}...")
-            samples.append(ingest.pack_sample(ref, paf, args.READS))
+            samples.append(ingest.pack_sample(ref, paf, reads))
             statprint("There were {} mapped reads.".format(samples[-1]["n_alignments"]))
+        t1 = time.perf_counter()
+        tm["ingest"] = t1 - t0
         if args.MIN_DEPTH_FACTOR is None:
             raise ingest.IngestError("TypeError: --min_depth_factor is required")  # max_depth*None (:338)
         gtf = args.GLOBAL_THRESHOLD_FACTOR
         statprint("Pileup and consensus on device {}...".format(args.device))
         results = engine.pileup(samples, args.MIN_DEPTH_FACTOR, 1.0 if gtf is None else gtf, device=args.device)
+        tm["device"] = time.perf_counter() - t1
         if gtf is None and any(len(r["count"]) or r["max_depth"] for r in results):
             raise ingest.IngestError("TypeError: --global_threshold_factor is required")  # (:421)
     except (ingest.IngestError, engine.DataError, OSError, UnicodeDecodeError) as e:
         print("Error: {}".format(e), file=sys.stderr)
         return 1
-    for (ref, paf, c, ch, acc), res in zip(jobs, results):
+    t2 = time.perf_counter()
+    for (ref, paf, _, c, ch, acc), res in zip(jobs, results):
         statprint("Max depth is {}.".format(res["max_depth"]))
         statprint("DEPTH_THRESHOLD is {}.".format(res["max_depth"] * args.MIN_DEPTH_FACTOR))
         statprint("Writing consensus, chromatogram data and per-position consensus accuracies...")
@@ -96,6 +114,7 @@ def main(argv=None):
         except OSError as e:  # WriteError included: the reference's open()/write() raise -> exit 1
             print("Error: {}".format(e), file=sys.stderr)
             return 1
+    tm["write"] = time.perf_counter() - t2
     for src, dst in args.revcomp:
         statprint("Reverse-complementing {} into {}...".format(src, dst))
         try:

@@ -72,14 +72,20 @@ def wgz(path, data):
             f.write(data)
 
 
-def run_case(name, script, core):
+def run_case(name, script, core, repeats=1, golden=True):
+    """Run the case's reference jobs; the first (mdf, gtf) run is timed
+    ``repeats`` times (median and spread recorded), the outputs of the first
+    repetition become the depth goldens (unless ``golden`` is False)."""
     cfg, kw, (a, b), full, strands, runs = CASES[name]
     syn = synth.Synth(reads=(a, b), **kw)
     aligned = int(sum(int(syn.sample(s)["aligned"].sum()) for s in range(strands)))
     cdir = os.path.join(GOLDEN, name)
-    if os.path.exists(cdir):
-        shutil.rmtree(cdir)
-    os.makedirs(cdir)
+    if golden:
+        if os.path.exists(cdir):
+            shutil.rmtree(cdir)
+        os.makedirs(cdir)
+    else:
+        runs = runs[:1]
     manifest = {"config": cfg, "synth": kw, "reads": [a, b], "strands": strands, "runs": []}
     walls = []
     with tempfile.TemporaryDirectory() as tmp:
@@ -87,8 +93,10 @@ def run_case(name, script, core):
         syn.write_files(p("ref.fa"), p("reads.fa"), p("s0.paf"), p("ref1.fa") if strands > 1 else None,
                         p("s1.paf") if strands > 1 else None)
         env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
-        for k, (mdf, gtf) in enumerate(runs):
+        plan = [(k, mdf, gtf, rep) for k, (mdf, gtf) in enumerate(runs) for rep in range(repeats if k == 0 else 1)]
+        for k, mdf, gtf, rep in plan:
             ent = {"mdf": mdf, "gtf": gtf, "strands": []}
+            job_wall = 0.0
             for s in range(strands):
                 ref = p("ref.fa") if s == 0 else p("ref1.fa")
                 cmd = ["taskset", "-c", str(core), sys.executable, "-B", script, "--ref", ref, "--reads", p("reads.fa"),
@@ -100,27 +108,36 @@ def run_case(name, script, core):
                 wall = time.perf_counter() - t0
                 if r.returncode != 0:
                     raise SystemExit(f"{name}: reference exit {r.returncode}: {r.stderr[-400:]}")
-                if k == 0:
-                    walls.append(wall)
+                job_wall += wall
+                print(f"{name} run{k} rep{rep} strand{s}: {wall:.2f} s", flush=True)
+                if rep or not golden:
+                    continue
                 files = {}
                 for f in ("c.fa", "ch.tsv", "acc.tsv"):
                     fn = f"run{k}_s{s}_{f}.gz"
                     wgz(os.path.join(cdir, fn), open(p(f), "rb").read())
                     files[f] = fn
                 ent["strands"].append({"files": files, "wall_s": round(wall, 3)})
-                print(f"{name} run{k} strand{s}: {wall:.2f} s", flush=True)
-            manifest["runs"].append(ent)
-    with open(os.path.join(cdir, "case.json"), "w") as f:
-        json.dump(manifest, f, indent=1, sort_keys=True)
-    wall = sum(walls)
+            if k == 0:
+                walls.append(job_wall)
+            if rep == 0:
+                manifest["runs"].append(ent)
+    if golden:
+        with open(os.path.join(cdir, "case.json"), "w") as f:
+            json.dump(manifest, f, indent=1, sort_keys=True)
+    ws = sorted(walls)
+    wall = ws[len(ws) // 2] if len(ws) % 2 else 0.5 * (ws[len(ws) // 2 - 1] + ws[len(ws) // 2])
     frac = (b - a) / full
     return cfg, {
         "value": aligned / wall, "unit": "aligned bases/s", "cores": 1, "kind": "reference",
-        "wall_s": round(wall, 3), "aligned_bases": aligned, "strand_jobs": strands,
+        "wall_s": round(wall, 3), "walls_s": [round(w, 3) for w in walls], "repeats": len(walls),
+        "spread": round((ws[-1] - ws[0]) / wall, 4),
+        "aligned_bases": aligned, "strand_jobs": strands,
         "extrapolated": frac < 1.0,
         "sample": (f"{name}: reads [{a}, {b}) of the {full}-read {cfg} set ({100 * frac:g} %), "
                    f"{strands} strand job(s) run one after the other (Snakefile:401-423), "
-                   f"/root/reference/src/mapped_paf_read_parser.py whole script, taskset -c {core}"
+                   f"/root/reference/src/mapped_paf_read_parser.py whole script, taskset -c {core}, "
+                   f"median of {len(walls)} run(s)"
                    + ("; rate extrapolated linearly to the full set (SURVEY §8(d))" if frac < 1.0 else "")),
     }
 
@@ -130,6 +147,8 @@ def main():
     ap.add_argument("--ref-script", default="/root/reference/src/mapped_paf_read_parser.py")
     ap.add_argument("--core", type=int, default=0)
     ap.add_argument("--only", nargs="*")
+    ap.add_argument("--repeats", type=int, default=3, help="timed repetitions per case (median recorded)")
+    ap.add_argument("--no-golden", action="store_true", help="time only; leave tests/golden_depth untouched")
     a = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
     rec = json.load(open(RECORD)) if os.path.exists(RECORD) else {}
@@ -137,7 +156,7 @@ def main():
                    "where": "build container (the reference does not exist on the GPU box)"}
     rec.setdefault("configs", {})
     for name in a.only or CASES:
-        cfg, r = run_case(name, a.ref_script, a.core)
+        cfg, r = run_case(name, a.ref_script, a.core, a.repeats, not a.no_golden)
         rec["configs"][cfg] = r
         with open(RECORD, "w") as f:
             json.dump(rec, f, indent=1, sort_keys=True)

@@ -22,6 +22,8 @@ pytestmark = pytest.mark.gpu
 
 SPECS = {
     "c2like": dict(n=2686, n_reads=24_000, profile="default", seed=2, frac_partial=0.05),
+    # >= 250k reads per strand over 2 processes: 125k reads per rank and strand
+    "c2_250k": dict(n=2686, n_reads=250_000, profile="default", seed=2, frac_partial=0.02),
     "partial_indel": dict(n=900, n_reads=6_000, profile="indel", seed=71, frac_partial=0.5, flank=(0, 60),
                           ins_len=(1, 8), del_len=(1, 6)),
 }
@@ -62,7 +64,7 @@ def _worker(rank, world, port, spec_name, q):
 
 
 @pytest.mark.timeout(300)
-@pytest.mark.parametrize("spec_name,world", [("c2like", 2), ("partial_indel", 3)])
+@pytest.mark.parametrize("spec_name,world", [("c2like", 2), ("partial_indel", 3), ("c2_250k", 2)])
 def test_dist_exchange_real_plans(pkg, spec_name, world):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
@@ -88,3 +90,27 @@ def test_dist_exchange_real_plans(pkg, spec_name, world):
         for (mdf, gtf), got in zip(((-1.0, 1.0), (0.1, 5.0)), out):
             for s, (g, f) in enumerate(zip(got, full)):
                 du.compare(g, du.derive(f, mdf, gtf), (spec_name, world, rank, s, mdf))
+
+
+@pytest.mark.timeout(900)
+def test_c3_eight_shards_in_process(pkg):
+    """BASELINE configs[2] (C3: 10 kb, 1M reads, sense) exactly as bench.py
+    --gpus 8 splits it -- 8 contiguous shards of ONE global read order -- with
+    the 8 shards' plans on this GPU and the exchanges in-process
+    (LocalExchange).  Every shard must end with the single-pileup result,
+    bit-exact with the C oracle, at full pileup and at 0.1 / 5.  The run replay
+    at mixed gaps depends on the global read order (mapped_paf_read_parser.py:292,
+    :37-72), so this pins the shard seams at size."""
+    bench = importlib.import_module("bench")
+    dist = importlib.import_module("minion-plasmid-consensus_amd.dist")
+    samples, total = bench.shard_samples(pkg, "c3", 0, 1)
+    assert total == 1_000_000 and len(samples) == 1
+    full = du.oracle_many(samples, -1.0, 1.0)
+    sp = dist.ShardedPileup(dist.split_samples(samples, 8), [0] * 8)
+    for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
+        sp.step(mdf, gtf)
+        sp.check()
+        for k, plan in enumerate(sp.plans):
+            for s, (got, f) in enumerate(zip(plan.fetch(), full)):
+                du.compare(got, du.derive(f, mdf, gtf), ("c3x8", k, s, mdf))
+    del sp

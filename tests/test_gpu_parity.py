@@ -40,6 +40,31 @@ def test_cli_matches_reference(case, tmp_path, cli):
             assert not any(os.path.exists(o) for o in outs), "no partial outputs on failure"
 
 
+def test_cli_jobs_own_reads_one_launch(tmp_path, cli):
+    """--job (a batch of plasmids, each with its OWN reads file, one launch):
+    every job's three files equal the reference's golden outputs of its case."""
+    cases = ["r01_default_sense", "r03_indel_antisense", "t2a_order", "r06_smallref_sense"]
+    argv, outs, exps = [], [], []
+    run_of = {}
+    for c in cases:
+        d = tmp_path / c
+        d.mkdir()
+        ref, reads, paf = gu.materialize(c, str(d))
+        k, run, exp = next(iter(gu.runs(c)))
+        run_of[c] = run
+        o = [str(d / f"o_{x}") for x in ("c.fa", "ch.tsv", "acc.tsv")]
+        argv += ["--job", ref, paf, reads, *o]
+        outs.append(o)
+        exps.append(exp)
+    mdfs = {(r["mdf"], r["gtf"]) for r in run_of.values()}
+    assert len(mdfs) == 1, mdfs  # one (mdf, gtf) per launch
+    mdf, gtf = mdfs.pop()
+    assert cli.main(argv + ["--min_depth_factor", repr(mdf), "--global_threshold_factor", repr(gtf)]) == 0
+    for c, o, exp in zip(cases, outs, exps):
+        for path, f in zip(o, ("c.fa", "ch.tsv", "acc.tsv")):
+            assert open(path, "rb").read() == exp[f], (c, f)
+
+
 @pytest.mark.parametrize("stem", ["r01_default", "r03_indel"])
 def test_cli_both_strands_one_launch(stem, tmp_path, cli):
     """--also (sense + antisense in one launch, same reads file) and --revcomp

@@ -174,6 +174,55 @@ def e2e_cli(pkg, cfg, reps=2):
         shutil.rmtree(tmp, ignore_errors=True)
 
 
+# what bounds K_parse by its counters (profiles/r03_stalls_*)
+LIMITER = ("latency/issue: far below the HBM roof; SQ counters in profiles/r03_stalls_c2, r03_stalls_c3 "
+           "(DESIGN.md §3)")
+
+
+def batch_l3_resident(cfg):
+    """Whether the kernel's input (cs + records) fits the 256 MiB Infinity Cache
+    between launches: then the FETCH counters and the achieved rate include L3 hits."""
+    n, reads, _, _, _, anti, _ = CONFIGS[cfg]
+    per_read = {"c1": 0.12, "c2": 0.12, "c3": 0.12, "c4": 0.53, "c5": 0.12}[cfg] * n + 24
+    samples = (C5_PER_GPU if cfg == "c5" else 1) * (2 if anti else 1)
+    return bool(per_read * reads * samples < 200e6)
+
+
+def kernel_roofline(pkg, eng, cfg, reps, torch):
+    """K_parse alone on ``cfg`` (device-resident), HIP events on its stream."""
+    samples, _ = shard_samples(pkg, cfg, 0, 1)
+    runner = eng.Runner(samples)
+    runner.step(0.1, 5.0)
+    runner.check()
+    plan, batch = runner.plan, runner.batch
+    stream = torch.cuda.current_stream()
+    for _ in range(2):
+        plan.profile_kernel(eng.K_PARSE)
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+    for a, b in ev:
+        a.record(stream)
+        plan.profile_kernel(eng.K_PARSE)
+        b.record(stream)
+    torch.cuda.synchronize()
+    k_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    alg = batch.cs_bytes + 24 * batch.n_reads
+    achieved = alg / (k_ms * 1e-3) / 1e9
+    traffic = None
+    try:
+        tr = json.load(open(os.path.join(REPO, "profiles", f"pmc_traffic_{cfg}.json")))
+        if tr.get("config") == cfg and tr.get("kernel") == "K_parse":
+            traffic = tr.get("hbm_bytes_per_launch")
+    except (OSError, ValueError):
+        pass
+    out = {"config": cfg, "bound": "hbm", "kernel": "K_parse", "achieved": achieved, "peak": HBM_PEAK_GBS,
+           "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "alg_bytes_per_launch": alg,
+           "mean_launch_us": k_ms * 1e3, "aligned_bases_per_launch": batch.aligned_bases,
+           "input_l3_resident": batch_l3_resident(cfg), "parse_geometry": plan.info()}
+    del runner, plan, batch
+    torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -183,6 +232,8 @@ def main():
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
+    ap.add_argument("--hbm-config", default="c3",
+                    help="also time K_parse on this (L3-exceeding) config for the HBM roofline; '' to skip")
     args = ap.parse_args()
 
     import torch
@@ -270,12 +321,25 @@ def main():
     except (OSError, ValueError):
         pass
 
-    cpu = e2e = None
+    cpu = e2e = hbm = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = port_baseline(samples, mdf, gtf, cfg)
-        cpu["reference"] = reference_record(cfg)
+        port = port_baseline(samples, mdf, gtf, cfg)
+        ref = reference_record(cfg)
+        if ref is not None:
+            # the reference script itself (kind "reference"; it cannot run on the GPU
+            # box, so it was timed in the build container: profiles/ref_cpu_baseline.json)
+            cpu = dict(ref, port=port)
+        else:
+            cpu = port
+    if rank == 0 and world == 1 and args.hbm_config and args.hbm_config != cfg:
+        # the same kernel on a workload that does NOT fit the 256 MiB Infinity
+        # Cache: C2's 71 MB of input stays L3-resident across launches, C3's 1.2 GB
+        # cannot -- the honest HBM fraction
+        del runner, plan
+        torch.cuda.empty_cache()
+        hbm = kernel_roofline(pkg, eng, args.hbm_config, args.kernel_reps, torch)
     if rank == 0 and world == 1 and not args.no_e2e and cfg in E2E_CONFIGS:
-        del runner, plan, batch
+        runner = plan = batch = None
         torch.cuda.empty_cache()
         e2e = e2e_cli(pkg, cfg)
 
@@ -294,7 +358,9 @@ def main():
                        "parallelism": ("replicas" if cfg == "c5" else "read-shard") + f"x{world}"},
             "roofline": {"bound": "hbm", "kernel": "K_parse", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
-                         "alg_bytes_per_launch": alg_bytes, "mean_launch_us": k_ms * 1e3},
+                         "alg_bytes_per_launch": alg_bytes, "mean_launch_us": k_ms * 1e3,
+                         "limiter": LIMITER, "input_l3_resident": batch_l3_resident(cfg)},
+            "roofline_hbm": hbm,
             "cpu_baseline": cpu,
             "e2e": e2e,
         }

@@ -209,6 +209,7 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
   int64_t cs_base, ovf_cap, read_offset, n_reads;
   int32_t nbs;       // bucket slots per parse workgroup (max buckets)
   int32_t* i_end; uint64_t* ins_raw; uint32_t* ins_sorted; int32_t* bk_cnt; int32_t* bk_off; int64_t* rbase;
+  int32_t* bk_cur;   // tally mode 4 only: per (workgroup, bucket) scatter cursors
   Ovf* ovf; uint32_t* ovf_cnt; uint32_t* hasleft; uint32_t* status;
   int32_t* diff; uint32_t* sub;
   // tally mode 3: substitutions as 2-byte events per (wave, position window),
@@ -225,11 +226,14 @@ constexpr int kSubWinBits = 14, kSubWin = 1 << kSubWinBits, kMaxSubWins = 4;
 __host__ __device__ inline int parse_hl_words(int n) { return (n + 1 + 31) / 32; }
 __host__ __device__ constexpr int parse_misc_bytes() { return kMaxPW * 4 + kMaxPW * 8; }
 template <int WIN>
-// position tallies of K_parse: 0 = global atomics, 1 = LDS, 12 B per position
+// position tallies of K_parse: 0 = global atomics, 4 = global atomics AND the
+// LEFT bitmap / insertion-bucket counters / event-sort cursors in HBM (references
+// too long for any LDS mode, up to kMaxRefLen), 1 = LDS, 12 B per position
 // (sub 4 x u16, depth decrements | increments u16), 2 = LDS, 10 B per position
 // (the depth difference as one biased 16-bit half), 3 = depth differences in
 // LDS (2 B per position), substitutions global: references up to ~40 kb
 __host__ __device__ inline int parse_lds_bytes(int n_max, int tm, int nbmax, int nw) {
+  if (tm == 4) return nw * (int)sizeof(WaveLds<WIN>) + parse_misc_bytes();  // per-gap state in HBM
   const int tallies = tm == 0 ? 0 : tm == 1 ? 12 * (n_max + 1) : tm == 2 ? 8 * (n_max + 1) + 4 * ((n_max + 2) / 2)
                                                                  : 4 * ((n_max + 2) / 2);
   const int buckets = 16 * nbmax + 4;  // epilogue: counts, cursors, chunk counts, chunk offsets
@@ -241,7 +245,7 @@ __host__ __device__ inline int parse_lds_bytes(int n_max, int tm, int nbmax, int
 // at most 2 to a position's depth counters; modes 2 / 3 keep the depth
 // difference as one half biased by 0x8000 (|sum| <= 2 * 16383 < 0x8000),
 // mode 1 keeps decrements and increments apart (2 * 32767 < 2^16)
-__host__ __device__ constexpr int64_t wg_reads_cap(int tm) { return tm >= 2 ? 16383 : 32767; }
+__host__ __device__ constexpr int64_t wg_reads_cap(int tm) { return tm == 2 || tm == 3 ? 16383 : 32767; }
 
 struct TokInfo { int adv; int kind; uint32_t pay; uint32_t err; };
 
@@ -434,7 +438,7 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, int64
                                int nreg, uint64_t* stg, int stg_cap) {
   constexpr bool fused = TM != 0;
   constexpr bool lds_sub = TM == 1 || TM == 2;
-  constexpr bool packed = TM >= 2;
+  constexpr bool packed = TM == 2 || TM == 3;
   const int l = lane();
   const int nsub = lds_sub ? 2 * (n + 1) : 0;
   const uint32_t* sub_l = uni;
@@ -549,6 +553,49 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, int64
   }
 }
 
+// Tally mode 4 (references beyond the LDS budget): the same bucket sort with
+// its counters in HBM.  The main loop counted every bucket's events into
+// bk_cur (zeroed by K_clear) with device atomics; one wave turns them into the
+// workgroup's bk_cnt / bk_off and scatter cursors, then every thread places its
+// raw events with a returning atomic on the cursor (K_left does not depend on
+// the order of a bucket's events, only on the slice they lie in).
+__device__ void parse_epilogue_big(const ParseArgs& a, int n, int nbk, int64_t r0, const uint32_t* wcnt,
+                                   const int64_t* wbase, int nreg) {
+  const int l = lane();
+  const int64_t wg = (int64_t)blockIdx.x * a.nbs;
+  const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;
+  if (threadIdx.x < 64) {  // every wave's counting atomics completed before the barrier
+    int carry_b = 0;
+    for (int c0 = 0; c0 < nbk; c0 += 64) {
+      const int k = c0 + l;
+      const int v = k < nbk ? __hip_atomic_load(a.bk_cur + wg + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+      const int inc = wave_scan_i32(v);
+      if (k < nbk) {
+        a.bk_cnt[wg + k] = v;
+        a.bk_off[wg + k] = carry_b + inc - v;
+        __hip_atomic_store(a.bk_cur + wg + k, carry_b + inc - v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      carry_b += wave_last_i32(inc);
+    }
+  }
+  if (threadIdx.x == 0) a.rbase[blockIdx.x] = rb_wg;
+  __syncthreads();
+  uint32_t* dst = a.ins_sorted + rb_wg;
+  const int64_t rg0 = a.read_offset + r0;
+  int Ev = 0;
+  for (int ww = 0; ww < nreg; ++ww) Ev += (int)wcnt[ww];
+  int ww_t = 0, pre_t = 0;
+  for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
+    while (k >= pre_t + (int)wcnt[ww_t]) { pre_t += (int)wcnt[ww_t]; ++ww_t; }
+    const uint64_t ev = a.ins_raw[wbase[ww_t] + (k - pre_t)];
+    const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
+    if (gap <= (uint32_t)n) {
+      const int pos = atomicAdd(a.bk_cur + wg + gap / kBW, 1);
+      dst[pos] = sorted_event(ev, rg0);
+    }
+  }
+}
+
 // Workgroup = contiguous reads of ONE sample (host work table); wave w takes
 // the w-th part of them and streams their cs bytes in windows of WIN bytes
 // (WIN/64 per lane, coalesced).  Token boundaries (special characters and read starts) are bits
@@ -588,9 +635,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int nbk = (n + 1 + kBW - 1) / kBW;  // insertion buckets
   uint32_t* bcnt = hl + parse_hl_words(n);  // [nbk] insertion events per bucket (counted as they are stored)
   uint32_t* uni = bcnt + nbk;
-  constexpr bool fused = TM != 0;           // depth differences in LDS (one address space per instantiation)
+  constexpr bool big = TM == 4;             // per-gap state (LEFT bitmap, bucket counters) in HBM
+  constexpr bool fused = TM >= 1 && TM <= 3;  // depth differences in LDS (one address space per instantiation)
   constexpr bool lds_sub = TM == 1 || TM == 2;  // substitution tallies in LDS too
-  constexpr bool packed = TM >= 2;
+  constexpr bool packed = TM == 2 || TM == 3;
   const int nsub = lds_sub ? 2 * (n + 1) : 0;
   uint32_t* sub_l = uni;                    // [2 (n+1)] (TM 1, 2): A | T << 16, C | G << 16
   // TM 1:    [n+1] depth-decrement count | depth-increment count << 16
@@ -598,7 +646,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   //          biased by 0x8000: at most 16383 reads per workgroup and 2 per read and
   //          position keep every partial sum inside (0, 0xffff): no carry across halves
   uint32_t* del_l = uni + nsub;
-  for (int k = threadIdx.x; k < parse_hl_words(n) + nbk; k += blockDim.x) hl[k] = 0;  // hl, bcnt
+  for (int k = threadIdx.x; !big && k < parse_hl_words(n) + nbk; k += blockDim.x) hl[k] = 0;  // hl, bcnt
   if (fused)
     for (int k = threadIdx.x; k < nsub + (packed ? (n + 2) / 2 : n + 1); k += blockDim.x)
       uni[k] = (packed && k >= nsub) ? 0x80008000u : 0u;
@@ -619,6 +667,14 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     else atomicAdd(a.diff + gb + pos, 1);
   };
 
+  auto left_bit = [&](int pos) {  // gap pos holds a LEFT event
+    if (big) atomicOr(a.hasleft + ((gb + pos) >> 5), 1u << ((gb + pos) & 31));
+    else atomicOr(hl + (pos >> 5), 1u << (pos & 31));
+  };
+  auto bucket_add = [&](int pos) {  // one more insertion event in pos's bucket
+    if (big) atomicAdd(a.bk_cur + (int64_t)blockIdx.x * a.nbs + pos / kBW, 1);
+    else atomicAdd(bcnt + pos / kBW, 1u);
+  };
   const int64_t ra = r0 + (r1 - r0) * w / nw, rb = r0 + (r1 - r0) * (w + 1) / nw;
   const int64_t wend = a.cs_off[rb];
   int64_t P = a.cs_off[ra];
@@ -729,7 +785,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if (up && ts > n) derr |= DE_INDEX;             // leftIndel(2*i) past the end
       if (o_nx <= cur.o) derr |= DE_OP;               // processOperation('', '')
       if (derr) flag_read(a, derr, rs0 + l);
-      if (up && ts >= 0 && ts <= n) atomicOr(hl + (ts >> 5), 1u << (ts & 31));  // upstream flank: LEFT at gap tstart
+      if (up && ts >= 0 && ts <= n) left_bit(ts);  // upstream flank: LEFT at gap tstart
       W.s_end[q] = o_nx;
       W.s_ts[q] = ts < 0 ? -1 : (ts > kICap ? kICap : ts);
       W.s_read[q] = (int32_t)(rs0 + l);
@@ -907,7 +963,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         depth_dec(i);
         depth_inc(i + olen_e < n ? i + olen_e : n);
       }
-      if (ok & (kind == 3)) atomicOr(hl + (i >> 5), 1u << (i & 31));
+      if (ok & (kind == 3)) left_bit(i);
       if (ok & (kind == 3) & (olen_e > kInsInline)) push_ovf(a, A + sx + 1, rl, i, olen_e);
       if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window
         const bool sev = te == 0 && kind == 2;
@@ -926,7 +982,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const uint64_t bins = ballot(ins_inline);
       if (ins_inline) {
         a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);
-        atomicAdd(bcnt + i / kBW, 1u);
+        bucket_add(i);
       }
       if (last) {  // the read's last operation: i_end, downstream check, span
         const int ia = i + adv;
@@ -974,8 +1030,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   MPC_SEG(5);
   __syncthreads();
   MPC_SEG(6);
-  parse_epilogue<TM>(a, n, gb, nbk, r0, hl, bcnt, uni, wcnt, wbase, nw, reinterpret_cast<uint64_t*>(lds),
-                     nw * (int)sizeof(WL) / 8);
+  if constexpr (big) parse_epilogue_big(a, n, nbk, r0, wcnt, wbase, nw);
+  else parse_epilogue<TM>(a, n, gb, nbk, r0, hl, bcnt, uni, wcnt, wbase, nw, reinterpret_cast<uint64_t*>(lds),
+                          nw * (int)sizeof(WL) / 8);
 #ifdef MPC_STAMPS
   MPC_SEG(7);
   const int64_t gw = (int64_t)blockIdx.x * kMaxPW + w;
@@ -2343,7 +2400,7 @@ struct mpc_plan {
     // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
     B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
     B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_SROW, B_WPARSE, B_WBC, B_UNITS, B_RUNT,
-    B_SUBEV, B_SUBCNT, B_WSUB, B_COUNT
+    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -2396,7 +2453,7 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.i_end = d.i_end;
   a.ins_raw = at<uint64_t>(p, mpc_plan::B_INSRAW); a.ins_sorted = at<uint32_t>(p, mpc_plan::B_INSSORT);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
-  a.rbase = at<int64_t>(p, mpc_plan::B_RBASE);
+  a.rbase = at<int64_t>(p, mpc_plan::B_RBASE); a.bk_cur = at<int32_t>(p, mpc_plan::B_BKCUR);
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.hasleft = d.hasleft; a.status = d.status;
   a.diff = d.diff; a.sub = d.sub;
   a.subev = at<uint16_t>(p, mpc_plan::B_SUBEV); a.subev_cnt = at<uint32_t>(p, mpc_plan::B_SUBCNT);
@@ -2406,6 +2463,7 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
 
 // instantiated (tally mode, window) pairs; packed modes only with 1 and 2 KiB windows
 static const void* parse_kernel(int tm, int win) {
+  if (tm == 4) return (const void*)K_parse<4, 1024>;
   if (tm == 2) return win == 1024 ? (const void*)K_parse<2, 1024> : (const void*)K_parse<2, 2048>;
   if (tm == 3) return win == 1024 ? (const void*)K_parse<3, 1024> : (const void*)K_parse<3, 2048>;
   if (win == 512) return tm ? (const void*)K_parse<1, 512> : (const void*)K_parse<0, 512>;
@@ -2425,7 +2483,8 @@ static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
   const dim3 g(p->n_parse_wg), b(p->parse_nw * 64);
   const ParseArgs a = parse_args(p, d);
   const int tm = p->tally_mode, win = p->parse_win;
-  if (tm == 2 && win == 1024) hipLaunchKernelGGL((K_parse<2, 1024>), g, b, p->parse_lds, st, a);
+  if (tm == 4) hipLaunchKernelGGL((K_parse<4, 1024>), g, b, p->parse_lds, st, a);
+  else if (tm == 2 && win == 1024) hipLaunchKernelGGL((K_parse<2, 1024>), g, b, p->parse_lds, st, a);
   else if (tm == 2) hipLaunchKernelGGL((K_parse<2, 2048>), g, b, p->parse_lds, st, a);
   else if (tm == 3 && win == 1024) hipLaunchKernelGGL((K_parse<3, 1024>), g, b, p->parse_lds, st, a);
   else if (tm == 3) hipLaunchKernelGGL((K_parse<3, 2048>), g, b, p->parse_lds, st, a);
@@ -2600,6 +2659,15 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
         const int score = wgs * nw * (c[1] == 512 ? 75 : c[1] == 1024 ? 95 : 100);
         if (score > best) { best = score; p->tally_mode = c[0]; p->parse_win = c[1]; p->parse_nw = nw; per_cu = wgs; }
       }
+    if (best < 0) {
+      // references beyond every LDS mode (~312 kb): per-gap parse state in HBM
+      for (int nw : {16, 12, 8}) {
+        const int lds = parse_lds_bytes<1024>((int)n_max, 4, p->nbmax, nw);
+        if (lds > lds_cap) continue;
+        const int wgs = std::max(1, std::min(lds_cap / lds, max_waves_cu / nw));
+        if (wgs * nw > best) { best = wgs * nw; p->tally_mode = 4; p->parse_win = 1024; p->parse_nw = nw; per_cu = wgs; }
+      }
+    }
     if (best < 0) { delete p; return fail(MPC_E_ARG, "reference too long for the LDS budget"); }
     p->parse_lds = lds_of(p->parse_win, p->tally_mode, p->parse_nw);
     // workgroups per sample: the smallest largest-chunk R with sum_s ceil(ns / R)
@@ -2730,6 +2798,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_SUBEV, p->subev_cap * p->sub_wins, 2);
   set(mpc_plan::B_SUBCNT, p->sub_wins ? (int64_t)p->n_parse_wg * kMaxPW * kMaxSubWins : 0, 4);
   set(mpc_plan::B_WSUB, (int64_t)p->work_sub.size(), 4);
+  set(mpc_plan::B_BKCUR, p->tally_mode == 4 ? (int64_t)p->n_parse_wg * p->nbmax : 0, 4);
   size_t o = 0;
   for (int b = 0; b < mpc_plan::B_COUNT; ++b) {
     o = (o + 255) & ~(size_t)255;
@@ -2838,6 +2907,7 @@ int mpc_parse(mpc_plan* p, void* stream) {
     add(d.diff, p->G, 0u);
     add(d.sub, 4 * p->G, 0u);
     add(d.maxR, p->G, 0u);
+    if (p->tally_mode == 4) add(at<int32_t>(p, mpc_plan::B_BKCUR), (int64_t)p->n_parse_wg * p->nbmax, 0u);
     add(d.maxdepth, p->S, 0u);
     add(d.M, p->runs_cap, 0u);
     add(d.runR, p->runs_cap, 0u);

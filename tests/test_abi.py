@@ -71,10 +71,16 @@ def test_planner_geometry(pkg):
 
 
 def test_planner_reference_limit(pkg):
-    """The largest reference the planner takes (mpc.h: 312,575 bases, tally mode
-    0 with 512-byte windows), and the error one base beyond it (host-only)."""
+    """The longest reference whose parse state fits LDS (312,575 bases, tally
+    mode 0 with 512-byte windows); one base beyond it the parse keeps that state
+    in HBM (tally mode 4), up to the 32-bit coordinates' 2^20 - 2 (mpc.h); past
+    that mpc_plan_create fails (host-only)."""
     g = pkg.engine.geometry
     info = g([312_575], [12], 312_575 * 3)
     assert info["tally_mode"] == 0 and info["parse_lds_bytes"] <= 160 * 1024
+    big = g([312_576], [12], 312_576 * 3)
+    assert big["tally_mode"] == 4 and big["parse_lds_bytes"] <= 160 * 1024
+    top = g([(1 << 20) - 2], [12], (1 << 20) * 3)
+    assert top["tally_mode"] == 4
     with pytest.raises(pkg.engine.MpcError):
-        g([312_576], [12], 312_576 * 3)
+        g([(1 << 20) - 1], [12], (1 << 20) * 3)

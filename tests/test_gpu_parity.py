@@ -250,19 +250,29 @@ def test_dense_tokens_match_oracle(pkg, seed):
         _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("dense", seed, mdf))
 
 
-def test_max_reference_length(pkg):
-    """The longest reference one launch takes (include/mpc.h: 312,575 bases, the
-    planner's LDS budget for the parse state; 32-bit coordinates would allow
-    2^20 - 2): bit-exact full pileup at the limit, one base more is rejected."""
-    n = MAX_REF
-    syn = pkg.synth.Synth(n=n, n_reads=12, profile="default", seed=48, frac_partial=0.5, antisense=False)
-    smp = syn.sample(0)
-    assert len(smp["ref"]) == n
-    _cmp(pkg.engine.pileup([smp], -1.0, 1.0)[0], _oracle(smp, -1.0, 1.0), "max_ref")
-    long = dict(smp)
-    long["ref"] = np.concatenate([smp["ref"], np.frombuffer(b"A", dtype=np.uint8)])
+@pytest.mark.parametrize("n,mode", [(312_575, 0), (400_000, 4)])
+def test_long_reference(pkg, n, mode):
+    """The longest reference whose parse state fits LDS (312,575 bases, tally
+    mode 0) and a 400 kb one past it (tally mode 4: LEFT bitmap, insertion-bucket
+    counters and event-sort cursors in HBM): bit-exact full pileup and at the
+    pipeline's thresholds, against the oracle (the reference takes any length,
+    mapped_paf_read_parser.py:161-184)."""
+    syn = pkg.synth.Synth(n=n, n_reads=40, profile="default", seed=48, frac_partial=0.5, antisense=True)
+    samples = [syn.sample(0), syn.sample(1)]
+    assert len(samples[0]["ref"]) == n
+    plan = pkg.engine.Plan(pkg.engine.Batch(samples))
+    assert plan.info()["tally_mode"] == mode
+    for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
+        res = pkg.engine.pileup(samples, mdf, gtf)
+        for s, r in zip(samples, res):
+            _cmp(r, _oracle(s, mdf, gtf), ("long_ref", n, mdf))
+
+
+def test_reference_past_coordinate_limit(pkg):
+    """2^20 - 1 bases: beyond the 32-bit coordinate scheme (mpc.h), rejected."""
+    long = {"ref": np.zeros((1 << 20) - 1, dtype=np.uint8) + ord("A"), "cs": np.frombuffer(b"Z::1", np.uint8).copy(),
+            "cs_off": np.array([0, 4], np.int64), "tstart": np.array([0], np.int64),
+            "up": np.zeros(0, np.uint8), "up_off": np.zeros(2, np.int64), "down": np.zeros(0, np.uint8),
+            "down_off": np.zeros(2, np.int64)}
     with pytest.raises(pkg.engine.MpcError):
         pkg.engine.Plan(pkg.engine.Batch([long]))
-
-
-MAX_REF = 312_575

@@ -252,7 +252,7 @@ struct TokInfo { int adv; int kind; uint32_t pay; uint32_t err; };
 // Semantics of one token that do not depend on its coordinate, operand read
 // from HBM: the slow path for rare tokens (a token longer than the window,
 // long insertions / substitution operands, ':' operands that are not 1-4 plain digits).
-__device__ TokInfo analyze_long(const uint8_t* cs, int64_t s, int64_t e, bool is_last) {
+__device__ __noinline__ TokInfo analyze_long(const uint8_t* cs, int64_t s, int64_t e, bool is_last) {
   TokInfo r{0, 0, 0u, 0u};
   const uint32_t op = cs[s];
   if (!is_special(op)) { r.err = DE_OP; return r; }
@@ -282,7 +282,7 @@ __device__ TokInfo analyze_long(const uint8_t* cs, int64_t s, int64_t e, bool is
 }
 
 // first special character in cs[x0, bound) (x0 16-aligned), else bound: all lanes, 1 KiB per step
-__device__ int64_t scan_special_wave(const uint8_t* cs, int64_t x0, int64_t bound) {
+__device__ __noinline__ int64_t scan_special_wave(const uint8_t* cs, int64_t x0, int64_t bound) {
   for (int64_t x = x0; x < bound; x += 1024) {
     const int64_t y = x + 16 * lane();
     uint32_t m = 0;

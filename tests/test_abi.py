@@ -50,35 +50,44 @@ def test_ingest_library_exports_all(pkg):
 
 
 def test_planner_geometry(pkg):
-    """Host-only planning (no device work): which K_parse tally mode every
-    BASELINE config runs in, and the reads-per-workgroup cap that keeps the
-    16-bit LDS tallies exact (mpc_kernels.hip wg_reads_cap)."""
+    """Host-only planning (no device work): every BASELINE config runs K_parse
+    with its per-position state in LDS (tally modes 1-3), within the LDS and
+    wave budgets, and the reads-per-workgroup cap that keeps the 16-bit LDS
+    tallies exact (mpc_kernels.hip wg_reads_cap) holds."""
     g = pkg.engine.geometry
     c2 = g([2686, 2686], [100_000, 100_000], 63 << 20)
     assert c2["tally_mode"] == 1 and c2["max_reads_per_workgroup"] <= c2["reads_per_workgroup_cap"] == 32767
     c3 = g([10_000], [1_000_000], 1200 << 20)
-    assert c3["tally_mode"] == 3 and c3["max_reads_per_workgroup"] <= c3["reads_per_workgroup_cap"] == 16383
+    c4 = g([10_000] * 2, [100_000] * 2, 1070 << 20)
     c5 = g([30_000] * 24, [10_000] * 24, 24 * 3600 * 10_000 // 100)
-    assert c5["tally_mode"] == 3
-    m6 = g([6000, 6000], [100_000, 100_000], 150 << 20)  # 10-byte packed tallies between tm 1 and tm 3
-    assert m6["tally_mode"] == 2 and m6["parse_waves"] == 16
-    # the cap binds: 4.9 M tiny reads beside one 10 kb sample put 16383 reads in a workgroup
+    assert c5["tally_mode"] == 3  # 30 kb: only the 2-byte depth tallies fit beside the waves
+    # the cap binds: 4.9 M tiny reads beside one 10 kb sample fill workgroups to the cap
     st = g([10_000, 30], [100, 16383 * 300], 16383 * 300 * 12)
-    assert st["tally_mode"] == 3
-    assert st["max_reads_per_workgroup"] == st["reads_per_workgroup_cap"] == 16383
-    for info in (c2, c3, c5, m6, st):
-        assert info["parse_lds_bytes"] <= 160 * 1024 and info["parse_waves"] in (8, 12, 16)
+    assert st["max_reads_per_workgroup"] == st["reads_per_workgroup_cap"]
+    for info in (c2, c3, c4, c5, st):
+        assert info["tally_mode"] in (1, 2, 3)
+        assert info["max_reads_per_workgroup"] <= info["reads_per_workgroup_cap"]
+        assert info["reads_per_workgroup_cap"] == (32767 if info["tally_mode"] == 1 else 16383)
+        assert info["parse_lds_bytes"] <= 160 * 1024 and info["parse_waves"] in (8, 10, 12, 16)
 
 
 def test_planner_reference_limit(pkg):
-    """The longest reference whose parse state fits LDS (312,575 bases, tally
-    mode 0 with 512-byte windows); one base beyond it the parse keeps that state
-    in HBM (tally mode 4), up to the 32-bit coordinates' 2^20 - 2 (mpc.h); past
-    that mpc_plan_create fails (host-only)."""
+    """The longest reference whose parse state fits LDS (tally mode 0 with the
+    fewest waves; ~314 kb); one base beyond it the parse keeps that state in HBM
+    (tally mode 4), up to the 32-bit coordinates' 2^20 - 2 (mpc.h); past that
+    mpc_plan_create fails (host-only)."""
     g = pkg.engine.geometry
-    info = g([312_575], [12], 312_575 * 3)
+    lo, hi = 100_000, 1_000_000  # bisect the last LDS-state length
+    while hi - lo > 1:
+        mid = (lo + hi) // 2
+        if g([mid], [12], mid * 3)["tally_mode"] == 4:
+            hi = mid
+        else:
+            lo = mid
+    assert 250_000 < lo < 400_000, lo
+    info = g([lo], [12], lo * 3)
     assert info["tally_mode"] == 0 and info["parse_lds_bytes"] <= 160 * 1024
-    big = g([312_576], [12], 312_576 * 3)
+    big = g([lo + 1], [12], (lo + 1) * 3)
     assert big["tally_mode"] == 4 and big["parse_lds_bytes"] <= 160 * 1024
     top = g([(1 << 20) - 2], [12], (1 << 20) * 3)
     assert top["tally_mode"] == 4

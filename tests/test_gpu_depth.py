@@ -21,7 +21,6 @@ import depth_util as du
 pytestmark = pytest.mark.gpu
 
 CONFIG_CASES = ["c1", "c2", "c3", "c4", "c5_slice", "c5"]
-EXPECT_MODE = {"c1": 1, "c2": 1, "c3": 3, "c4": 3, "c5_slice": 3, "c5": 3}
 
 
 def _samples(pkg, case):
@@ -57,7 +56,7 @@ def _check(pkg, samples, tag, mode=None):
 @pytest.mark.parametrize("case", CONFIG_CASES)
 def test_config_full_size(pkg, case):
     samples = _samples(pkg, case)
-    _check(pkg, samples, case, EXPECT_MODE[case])
+    _check(pkg, samples, case)
 
 
 def _tiny_reads_batch(pkg, n_tiny, big_n, big_reads=100):
@@ -72,11 +71,13 @@ def _tiny_reads_batch(pkg, n_tiny, big_n, big_reads=100):
 
 
 @pytest.mark.timeout(600)
-@pytest.mark.parametrize("big_n,mode", [(6_000, 2), (10_000, 3)])
-def test_workgroup_cap_packed_tallies(pkg, big_n, mode):
+@pytest.mark.parametrize("mode", [2, 3])
+def test_workgroup_cap_packed_tallies(pkg, mode):
     """Tally modes 2 (10-byte packed LDS tallies) and 3 (LDS depth, substitution
-    events: C3 / C4 / C5): 16383 reads per workgroup."""
-    samples = _tiny_reads_batch(pkg, 16383 * 300, big_n)
+    events): 16383 reads per workgroup (the reference length that puts the
+    planner in each mode: tests/geometry_util.py)."""
+    import geometry_util as geo
+    samples = _tiny_reads_batch(pkg, 16383 * 300, geo.first_length(mode))
     info = pkg.engine.Plan(pkg.engine.Batch(samples)).info()
     assert info["tally_mode"] == mode and info["max_reads_per_workgroup"] == info["reads_per_workgroup_cap"] == 16383
     _check(pkg, samples, "cap_tm%d" % mode, mode)

@@ -11,6 +11,7 @@ import os
 import numpy as np
 import pytest
 
+import geometry_util as geo
 import golden_util as gu
 import oracle
 
@@ -118,25 +119,25 @@ SYNTH = [
     dict(n=50, n_reads=2000, profile="c1probe", seed=7, frac_partial=0.5, flank=(0, 8)),
     dict(n=3000, n_reads=500, profile="default", seed=9, frac_partial=0.3, ins_len=(1, 1500), del_len=(1, 1200),
          p_ins=0.0005, p_del=0.0005, flank=(0, 3000)),
-    # K_parse geometry by reference length (planner, mpc_plan_info): ~6 kb ->
-    # packed 10-byte LDS tallies (tally mode 2); 10-45 kb -> LDS depth +
-    # substitution events in 16384-position windows (mode 3: 1 and 3 windows);
-    # ~70 kb -> global-atomic tallies (mode 0)
-    dict(n=6000, n_reads=1000, profile="default", seed=43, frac_partial=0.2),
-    dict(n=10000, n_reads=1200, profile="indel", seed=44, frac_partial=0.2),
-    dict(n=20000, n_reads=300, profile="default", seed=45, frac_partial=0.3),
-    dict(n=45000, n_reads=120, profile="indel", seed=47, frac_partial=0.3),
-    dict(n=70000, n_reads=60, profile="default", seed=46, frac_partial=0.3),
+    # every K_parse tally mode the planner uses (tests/geometry_util.py): the
+    # shortest reference in each LDS mode, mode 3 also with 3 substitution
+    # windows (> 2 x 16384 positions), and the global-atomic mode 0
 ]
-SYNTH_MODE = {6000: 2, 10000: 3, 20000: 3, 45000: 3, 70000: 0}
+SYNTH += [dict(n=geo.first_length(m), n_reads=1000, profile="default" if m != 3 else "indel", seed=43 + m,
+               frac_partial=0.2) for m in (1, 2, 3)]
+SYNTH += [dict(n=geo.first_length(3, 2 * 16384), n_reads=150, profile="indel", seed=47, frac_partial=0.3),
+          dict(n=geo.first_length(0), n_reads=60, profile="default", seed=46, frac_partial=0.3)]
+
+
+def test_every_tally_mode_planned():
+    """The planner still reaches every mode at some reference length."""
+    assert {0, 1, 2, 3} <= set(geo.mode_lengths())
 
 
 @pytest.mark.parametrize("spec", SYNTH, ids=lambda s: f"n{s['n']}_N{s['n_reads']}_{s['profile']}_s{s['seed']}")
 def test_synthetic_full_pileup(pkg, spec):
     syn = pkg.synth.Synth(**spec)
     samples = [syn.sample(0), syn.sample(1)]
-    if spec["n"] in SYNTH_MODE:
-        assert pkg.engine.Plan(pkg.engine.Batch(samples)).info()["tally_mode"] == SYNTH_MODE[spec["n"]]
     for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0), (0.5, 2.5)):
         res = pkg.engine.pileup(samples, mdf, gtf)
         for s, (smp, r) in enumerate(zip(samples, res)):
@@ -250,12 +251,12 @@ def test_dense_tokens_match_oracle(pkg, seed):
         _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("dense", seed, mdf))
 
 
-@pytest.mark.parametrize("n,mode", [(312_575, 0), (400_000, 4)])
+@pytest.mark.parametrize("n,mode", [(300_000, 0), (400_000, 4)])
 def test_long_reference(pkg, n, mode):
-    """The longest reference whose parse state fits LDS (312,575 bases, tally
-    mode 0) and a 400 kb one past it (tally mode 4: LEFT bitmap, insertion-bucket
-    counters and event-sort cursors in HBM): bit-exact full pileup and at the
-    pipeline's thresholds, against the oracle (the reference takes any length,
+    """A 300 kb reference (parse state in LDS, tally mode 0) and a 400 kb one
+    past the LDS budget (tally mode 4: LEFT bitmap, insertion-bucket counters
+    and event-sort cursors in HBM): bit-exact full pileup and at the pipeline's
+    thresholds, against the oracle (the reference takes any length,
     mapped_paf_read_parser.py:161-184)."""
     syn = pkg.synth.Synth(n=n, n_reads=40, profile="default", seed=48, frac_partial=0.5, antisense=True)
     samples = [syn.sample(0), syn.sample(1)]

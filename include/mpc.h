@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MPC_ABI_VERSION 5
+#define MPC_ABI_VERSION 6
 
 /* return codes */
 #define MPC_OK 0
@@ -100,6 +100,11 @@ typedef struct {
   int64_t n_reads_global;
   int32_t shard;               /* this shard's index */
   int32_t n_shards;            /* number of shards (0 is taken as 1) */
+  /* optional host copy of cs_off ([n_reads+1], same values as the device one):
+   * the planner then splits the parse work (workgroups and the waves inside
+   * them) by cs BYTES instead of by read count, so no wave waits for a longer
+   * neighbour at the end of the parse.  NULL: split by read count. */
+  const int64_t* h_cs_off;
 } mpc_input;
 
 typedef struct mpc_plan mpc_plan;

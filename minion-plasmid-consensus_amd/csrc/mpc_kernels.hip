@@ -206,6 +206,7 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
   const uint8_t* cs; const int64_t* cs_off; const int32_t* tstart;
   const int64_t* up_off; const int64_t* down_off; const int32_t* n_of; const int32_t* gbase;
   const int4* work;  // per workgroup: {sample, first read, end read, 0}
+  const int32_t* wave_tab;  // per workgroup: kMaxPW + 1 read boundaries of its waves (planner: by cs bytes)
   int64_t cs_base, ovf_cap, read_offset, n_reads;
   int32_t nbs;       // bucket slots per parse workgroup (max buckets)
   int32_t* i_end; uint64_t* ins_raw; uint32_t* ins_sorted; int32_t* bk_cnt; int32_t* bk_off; int64_t* rbase;
@@ -675,7 +676,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     if (big) atomicAdd(a.bk_cur + (int64_t)blockIdx.x * a.nbs + pos / kBW, 1);
     else atomicAdd(bcnt + pos / kBW, 1u);
   };
-  const int64_t ra = r0 + (r1 - r0) * w / nw, rb = r0 + (r1 - r0) * (w + 1) / nw;
+  // this wave's reads: the planner's split of the workgroup's reads by cs bytes
+  const int32_t* wt = a.wave_tab + (int64_t)blockIdx.x * (kMaxPW + 1);
+  const int64_t ra = wt[w], rb = wt[w + 1];
   const int64_t wend = a.cs_off[rb];
   int64_t P = a.cs_off[ra];
   const int64_t ev_base = (P - a.cs_base) / 2 + 3 * ra;  // this wave's event region in ins_raw
@@ -1059,6 +1062,7 @@ constexpr int kSubsWG = 32;  // parse workgroups per K_subs block, at most
 struct SubsArgs {
   const int4* work;    // {sample, window, first parse workgroup, end}
   const int4* pwork;   // parse work table {sample, r0, r1, 0}
+  const int32_t* wave_tab;  // the parse waves' read ranges (kMaxPW + 1 boundaries per workgroup)
   const int64_t* cs_off; int64_t cs_base;
   const uint16_t* subev; const uint32_t* subev_cnt; int64_t subev_cap;
   const int32_t* n_of; const int32_t* gbase; uint32_t* sub;
@@ -1073,8 +1077,7 @@ __global__ __launch_bounds__(1024) void K_subs(SubsArgs a) {
   __syncthreads();
   for (int rg = v; rg < nreg; rg += nv) {
     const int pw = pw0 + rg / a.nw_parse, ww = rg % a.nw_parse;
-    const int4 pk = a.pwork[pw];
-    const int64_t ra = pk.y + (int64_t)(pk.z - pk.y) * ww / a.nw_parse;
+    const int64_t ra = a.wave_tab[(int64_t)pw * (kMaxPW + 1) + ww];  // the parse wave's first read
     const int c = (int)a.subev_cnt[((int64_t)pw * kMaxPW + ww) * kMaxSubWins + win];
     const uint16_t* src = a.subev + (int64_t)win * a.subev_cap + (a.cs_off[ra] - a.cs_base) / 3 + 2 * ra;
     for (int e0 = 0; e0 < c; e0 += 8 * 64) {
@@ -2387,6 +2390,7 @@ struct mpc_plan {
   size_t ws_bytes = 0;
   uint8_t* ws = nullptr;
   std::vector<int32_t> work_parse, work_bc, work_sub;  // int4 records
+  std::vector<int32_t> work_wave;                     // per parse workgroup: kMaxPW + 1 wave boundaries
   int32_t sub_wins = 0;                               // tally mode 3: substitution-event windows
   int64_t subev_cap = 0;
   int n_parse_wg = 0, parse_lds = 0, nbmax = 1, parse_win = 1024, parse_nw = 8;
@@ -2400,7 +2404,7 @@ struct mpc_plan {
     // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
     B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
     B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_SROW, B_WPARSE, B_WBC, B_UNITS, B_RUNT,
-    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_COUNT
+    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -2448,6 +2452,7 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.cs = d.cs; a.cs_off = d.cs_off; a.tstart = d.tstart; a.up_off = d.up_off; a.down_off = d.down_off;
   a.n_of = d.n_of; a.gbase = d.gbase;
   a.work = reinterpret_cast<const int4*>(p->ws + p->off[mpc_plan::B_WPARSE]);
+  a.wave_tab = at<const int32_t>(p, mpc_plan::B_WWAVE);
   a.cs_base = d.cs_base; a.ovf_cap = d.ovf_cap; a.read_offset = d.read_offset; a.n_reads = d.N;
   a.nbs = p->nbmax;
   a.i_end = d.i_end;
@@ -2477,6 +2482,7 @@ static void launch_subs(const mpc_plan* p, const Dev& d, hipStream_t st) {
   a.cs_off = d.cs_off; a.cs_base = d.cs_base;
   a.subev = at<uint16_t>(p, mpc_plan::B_SUBEV); a.subev_cnt = at<uint32_t>(p, mpc_plan::B_SUBCNT);
   a.subev_cap = p->subev_cap; a.n_of = d.n_of; a.gbase = d.gbase; a.sub = d.sub; a.nw_parse = p->parse_nw;
+  a.wave_tab = at<const int32_t>(p, mpc_plan::B_WWAVE);
   hipLaunchKernelGGL(K_subs, dim3((unsigned)(p->work_sub.size() / 4)), dim3(1024), 0, st, a);
 }
 static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
@@ -2688,17 +2694,44 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       for (int s = 0; s < p->S; ++s) tot += chunks(p->read_begin[s + 1] - p->read_begin[s], mid);
       if (tot <= target) R_hi = mid; else R_lo = mid + 1;
     }
+    // boundaries of [a, b) cut into k parts: equal cs BYTES when the host copy
+    // of cs_off is given (the parse time of a read range follows its bytes, not
+    // its read count: a count split left waves idle at the epilogue barrier 22 %
+    // of their time, profiles/r03_stamps), else equal read counts
+    const int64_t* hco = in->h_cs_off;
+    auto cut = [&](int64_t a, int64_t b, int64_t k, std::vector<int64_t>& out) {
+      out.assign((size_t)k + 1, a);
+      out[(size_t)k] = b;
+      for (int64_t c = 1; c < k; ++c) {
+        int64_t x = a + (b - a) * c / k;
+        if (hco) {
+          const int64_t tgt = hco[a] + (hco[b] - hco[a]) * c / k;
+          x = std::lower_bound(hco + a, hco + b + 1, tgt) - hco;
+        }
+        out[(size_t)c] = std::min(std::max(x, out[(size_t)c - 1]), b);
+      }
+    };
+    std::vector<int64_t> bnd;
     std::vector<int> pw_begin(p->S + 1, 0);
     for (int s = 0; s < p->S; ++s) {
       pw_begin[s] = (int)(p->work_parse.size() / 4);
       const int64_t a = p->read_begin[s], b = p->read_begin[s + 1], ns = b - a;
       if (ns <= 0) continue;
       const int64_t ch = chunks(ns, R_lo);
+      cut(a, b, ch, bnd);
+      bool capped = true;  // the byte split must keep the 16-bit tallies' reads-per-workgroup cap
+      for (int64_t c = 0; c < ch; ++c) capped &= bnd[(size_t)c + 1] - bnd[(size_t)c] <= wcap;
       for (int64_t c = 0; c < ch; ++c) {
-        const int64_t x = a + ns * c / ch, y = a + ns * (c + 1) / ch;
+        const int64_t x = capped ? bnd[(size_t)c] : a + ns * c / ch;
+        const int64_t y = capped ? bnd[(size_t)c + 1] : a + ns * (c + 1) / ch;
         if (y > x) p->work_parse.insert(p->work_parse.end(), {s, (int32_t)x, (int32_t)y, 0});
         p->max_wg_reads = std::max<int64_t>(p->max_wg_reads, y - x);
       }
+    }
+    // the waves of every workgroup: contiguous read ranges, again by bytes
+    for (size_t k = 0; k < p->work_parse.size(); k += 4) {
+      cut(p->work_parse[k + 1], p->work_parse[k + 2], p->parse_nw, bnd);
+      for (int w = 0; w <= kMaxPW; ++w) p->work_wave.push_back((int32_t)bnd[(size_t)std::min(w, p->parse_nw)]);
     }
     pw_begin[p->S] = (int)(p->work_parse.size() / 4);
     p->n_parse_wg = pw_begin[p->S];
@@ -2799,6 +2832,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_SUBCNT, p->sub_wins ? (int64_t)p->n_parse_wg * kMaxPW * kMaxSubWins : 0, 4);
   set(mpc_plan::B_WSUB, (int64_t)p->work_sub.size(), 4);
   set(mpc_plan::B_BKCUR, p->tally_mode == 4 ? (int64_t)p->n_parse_wg * p->nbmax : 0, 4);
+  set(mpc_plan::B_WWAVE, (int64_t)p->work_wave.size(), 4);
   size_t o = 0;
   for (int b = 0; b < mpc_plan::B_COUNT; ++b) {
     o = (o + 255) & ~(size_t)255;
@@ -2806,6 +2840,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     o += p->sz[b];
   }
   p->ws_bytes = (o + 255) & ~(size_t)255;
+  p->in.h_cs_off = nullptr;  // host array only read while planning
   *out = p;
   return MPC_OK;
 }
@@ -2837,6 +2872,7 @@ int mpc_plan_set_input(mpc_plan* p, const mpc_input* in) {
   if (in->n_reads != p->N || in->n_samples != p->S || in->cs_bytes > p->in.cs_bytes)
     return fail(MPC_E_ARG, "input shape differs from the plan");
   p->in = *in;
+  p->in.h_cs_off = nullptr;  // the work split stays the one planned
   return MPC_OK;
 }
 
@@ -2854,6 +2890,9 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WPARSE), p->work_parse.data(), 4 * p->work_parse.size(), hipMemcpyHostToDevice));
   if (!p->work_bc.empty())
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WBC), p->work_bc.data(), 4 * p->work_bc.size(), hipMemcpyHostToDevice));
+  if (!p->work_wave.empty())
+    HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WWAVE), p->work_wave.data(), 4 * p->work_wave.size(),
+                     hipMemcpyHostToDevice));
   if (!p->work_sub.empty())
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WSUB), p->work_sub.data(), 4 * p->work_sub.size(), hipMemcpyHostToDevice));
   HIPCHK(hipFuncSetAttribute(parse_kernel(p->tally_mode, p->parse_win), hipFuncAttributeMaxDynamicSharedMemorySize,

@@ -14,7 +14,7 @@ from . import _build
 
 LIB_PATH = _build.LIBMPC
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED = 0, 1, 2, 3
 DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL = 1, 2, 4, 8, 16, 32
 (BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_CNT, BUF_RIGHT_CNT_ALL,
@@ -73,6 +73,7 @@ class _Input(ctypes.Structure):
         ("n_reads_global", ctypes.c_int64),
         ("shard", ctypes.c_int32),
         ("n_shards", ctypes.c_int32),
+        ("h_cs_off", ctypes.POINTER(ctypes.c_int64)),
     ]
 
 
@@ -155,7 +156,10 @@ class Batch:
     """Device-resident inputs of one launch: one or more samples (strands /
     plasmids) concatenated, reads grouped by sample."""
 
-    def __init__(self, samples, device=0, read_offset=0, n_reads_global=None, shard=0, n_shards=1):
+    def __init__(self, samples, device=0, read_offset=0, n_reads_global=None, shard=0, n_shards=1,
+                 balance_bytes=True):
+        """``balance_bytes``: hand the planner the host cs offsets so the parse
+        work is split by cs bytes (mpc.h h_cs_off); False splits by read count."""
         torch = _torch()
         if not torch.cuda.is_available():
             raise MpcError("no HIP device visible (the pileup path has no CPU fallback)")
@@ -210,12 +214,14 @@ class Batch:
             down=dev(dn, FLANK_PAD), down_off=dev(dn_off), sample=dev(sample),
         )
         self.h_cs_off = cs_off
+        self.balance_bytes = bool(balance_bytes)
         self.max_flank = int(max((np.diff(up_off).max() if len(up_off) > 1 else 0),
                                  (np.diff(dn_off).max() if len(dn_off) > 1 else 0)))
 
     def c_input(self):
         t = self.t
-        self._keep = (np.ascontiguousarray(self.ref_len), np.ascontiguousarray(self.read_begin))
+        self._keep = (np.ascontiguousarray(self.ref_len), np.ascontiguousarray(self.read_begin),
+                      np.ascontiguousarray(self.h_cs_off, dtype=np.int64))
         return _Input(
             ref=t["ref"].data_ptr(), ref_off=t["ref_off"].data_ptr(), cs=t["cs"].data_ptr(),
             cs_off=t["cs_off"].data_ptr(), tstart=t["tstart"].data_ptr(), up=t["up"].data_ptr(),
@@ -226,6 +232,8 @@ class Batch:
             n_reads=self.n_reads, cs_bytes=self.cs_bytes, cs_base=0,
             read_offset=self.read_offset, n_reads_global=self.n_reads_global,
             shard=self.shard, n_shards=self.n_shards,
+            h_cs_off=(self._keep[2].ctypes.data_as(ctypes.POINTER(ctypes.c_int64)) if self.balance_bytes
+                      else ctypes.POINTER(ctypes.c_int64)()),
         )
 
     def row_estimate(self):

@@ -137,6 +137,14 @@ const char* mpc_last_error(void);
  * caller re-plans with a larger row_cap.  Host-only, no device work. */
 int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** plan);
 int mpc_plan_destroy(mpc_plan* plan);
+/* Host copies of the parse work split (tests / tools; no device work):
+ * work   n_wg x {sample, first read, end read, chunks} (int32)
+ * chunks n_wg x (MPC_PARSE_CHUNKS + 1) read boundaries: the workgroup's reads cut
+ *        into contiguous chunks that its waves take in turn.
+ * Either pointer may be NULL.  Returns n_wg (>= 0) or a negative MPC_E_*. */
+#define MPC_PARSE_CHUNKS 48
+int mpc_plan_parse_tables(const mpc_plan* plan, int32_t* work, int32_t* chunks);
+
 int mpc_plan_workspace_bytes(const mpc_plan* plan, size_t* bytes);
 int mpc_plan_bind(mpc_plan* plan, void* workspace, size_t bytes);
 int mpc_plan_buffer(const mpc_plan* plan, int which, size_t* byte_offset, int64_t* count);

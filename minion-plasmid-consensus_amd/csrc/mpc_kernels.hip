@@ -183,6 +183,7 @@ __device__ uint64_t g_stamps[kStampWaves * kStampSeg];
 constexpr int kSlots = 64;              // reads touching a window (slot 0 = read carried in)
 constexpr int kMaxPW = 16;              // waves per workgroup (runtime: blockDim.x / 64)
 constexpr uint32_t kFar = 0x7fffu;      // sentinel: the window's only token ends beyond the window
+constexpr int kMaxCh = MPC_PARSE_CHUNKS;  // read chunks per parse workgroup, taken dynamically by its waves
 
 // units per window (tok list capacity): a 2 KiB window is cut early when it
 // would hold more (LDS budget), smaller windows never hold more than WIN
@@ -205,8 +206,8 @@ struct alignas(16) WaveLds {            // per-wave LDS of K_parse
 struct ParseArgs {  // slim argument block (no SGPR spills)
   const uint8_t* cs; const int64_t* cs_off; const int32_t* tstart;
   const int64_t* up_off; const int64_t* down_off; const int32_t* n_of; const int32_t* gbase;
-  const int4* work;  // per workgroup: {sample, first read, end read, 0}
-  const int32_t* wave_tab;  // per workgroup: kMaxPW + 1 read boundaries of its waves (planner: by cs bytes)
+  const int4* work;  // per workgroup: {sample, first read, end read, chunks}
+  const int32_t* wave_tab;  // per workgroup: kMaxCh + 1 read boundaries of its chunks (planner: by cs bytes)
   int64_t cs_base, ovf_cap, read_offset, n_reads;
   int32_t nbs;       // bucket slots per parse workgroup (max buckets)
   int32_t* i_end; uint64_t* ins_raw; uint32_t* ins_sorted; int32_t* bk_cnt; int32_t* bk_off; int64_t* rbase;
@@ -225,7 +226,9 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
 constexpr int kSubWinBits = 14, kSubWin = 1 << kSubWinBits, kMaxSubWins = 4;
 
 __host__ __device__ inline int parse_hl_words(int n) { return (n + 1 + 31) / 32; }
-__host__ __device__ constexpr int parse_misc_bytes() { return kMaxPW * 4 + kMaxPW * 8; }
+// per-chunk event counts and regions, the chunk table (read, cs offset), the chunk counter
+__host__ __device__ constexpr int parse_misc_bytes() { return kMaxCh * 4 + kMaxCh * 8 + (kMaxCh + 2) * 8 + (kMaxCh + 4) * 4 + 16; }
+static_assert(parse_misc_bytes() % 16 == 0 && kMaxCh % 4 == 0, "parse LDS misc area alignment");
 template <int WIN>
 // position tallies of K_parse: 0 = global atomics, 4 = global atomics AND the
 // LEFT bitmap / insertion-bucket counters / event-sort cursors in HBM (references
@@ -621,9 +624,12 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int nw = (int)(blockDim.x >> 6);
   const int w = uniform_i32((int)(threadIdx.x >> 6));
   WL& W = *reinterpret_cast<WL*>(lds + w * (int)sizeof(WL));
-  uint32_t* wcnt = reinterpret_cast<uint32_t*>(lds + nw * (int)sizeof(WL));     // [kMaxPW] events per wave
-  int64_t* wbase = reinterpret_cast<int64_t*>(wcnt + kMaxPW);                  // [kMaxPW] event region per wave
-  uint32_t* hl = reinterpret_cast<uint32_t*>(wbase + kMaxPW);                  // LEFT gaps bitmap
+  uint32_t* wcnt = reinterpret_cast<uint32_t*>(lds + nw * (int)sizeof(WL));     // [kMaxCh] events per chunk
+  int64_t* wbase = reinterpret_cast<int64_t*>(wcnt + kMaxCh);                  // [kMaxCh] event region per chunk
+  int64_t* cbo = wbase + kMaxCh;                                                // [kMaxCh + 1] chunk bounds: cs offset
+  int32_t* cbr = reinterpret_cast<int32_t*>(cbo + kMaxCh + 2);                  // [kMaxCh + 1] ... and read
+  uint32_t* cnext = reinterpret_cast<uint32_t*>(cbr + kMaxCh + 4);              // next chunk to take
+  uint32_t* hl = cnext + 4;                                                      // LEFT gaps bitmap
   const int4 wk = a.work[blockIdx.x];
 #ifdef MPC_STAMPS
   uint64_t st_acc[kStampSeg] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev;
@@ -648,6 +654,13 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   //          position keep every partial sum inside (0, 0xffff): no carry across halves
   uint32_t* del_l = uni + nsub;
   for (int k = threadIdx.x; !big && k < parse_hl_words(n) + nbk; k += blockDim.x) hl[k] = 0;  // hl, bcnt
+  if (threadIdx.x == 0) *cnext = (uint32_t)nw;  // chunks 0..nw-1 go to waves 0..nw-1
+  const int nch = wk.w;
+  for (int k = threadIdx.x; k <= nch; k += blockDim.x) {
+    const int32_t r = a.wave_tab[(int64_t)blockIdx.x * (kMaxCh + 1) + k];
+    cbr[k] = r;
+    cbo[k] = a.cs_off[r];
+  }
   if (fused)
     for (int k = threadIdx.x; k < nsub + (packed ? (n + 2) / 2 : n + 1); k += blockDim.x)
       uni[k] = (packed && k >= nsub) ? 0x80008000u : 0u;
@@ -676,12 +689,26 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     if (big) atomicAdd(a.bk_cur + (int64_t)blockIdx.x * a.nbs + pos / kBW, 1);
     else atomicAdd(bcnt + pos / kBW, 1u);
   };
-  // this wave's reads: the planner's split of the workgroup's reads by cs bytes
-  const int32_t* wt = a.wave_tab + (int64_t)blockIdx.x * (kMaxPW + 1);
-  const int64_t ra = wt[w], rb = wt[w + 1];
-  const int64_t wend = a.cs_off[rb];
-  int64_t P = a.cs_off[ra];
-  const int64_t ev_base = (P - a.cs_base) / 2 + 3 * ra;  // this wave's event region in ins_raw
+  // The workgroup's reads come in chunks (planner: contiguous, by cs bytes,
+  // 5/8 of the bytes in the first nw chunks, smaller ones after); wave w
+  // starts on chunk w and takes the next free one when it is done, so all
+  // waves reach the epilogue barrier within about one small chunk of each
+  // other (a static share per wave left them waiting there ~20 % of their
+  // time: profiles/r03_stamps).  The chunk table sits in LDS (one load per
+  // chunk bound per workgroup).  A chunk is a stream of its own: event
+  // regions, i_end.
+  // take the next chunk: every lane adds (lane 0 one, the others zero), so no
+  // divergent region guards the atomic (a lane-0-only atomic in the loop head
+  // was compiled into a loop exit that only lane 0 took: the wave never left)
+  auto take_chunk = [&]() {
+    const uint32_t v = atomicAdd(cnext, l == 0 ? 1u : 0u);
+    return uniform_i32(__builtin_amdgcn_readlane((int)v, 0));
+  };
+  for (int chk = w < nch ? w : nch; chk < nch; chk = take_chunk()) {
+  const int64_t ra = uniform_i32(cbr[chk]), rb = uniform_i32(cbr[chk + 1]);
+  const int64_t wend = readlane64(cbo[chk + 1], 0);
+  int64_t P = readlane64(cbo[chk], 0);
+  const int64_t ev_base = (P - a.cs_base) / 2 + 3 * ra;  // this chunk's event region in ins_raw
   const int64_t sev_base = (P - a.cs_base) / 3 + 2 * ra;  // ... and its substitution-event regions (TM 3)
   uint32_t nsub_v = 0;                                    // lane k: substitution events of window k
   uint32_t nev = 0;                                       // events written (wave-uniform)
@@ -1028,13 +1055,14 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     flag_read(a, DE_OP, r);
     a.i_end[r] = ts < 0 ? 0 : (ts > n ? n + 1 : ts);
   }
-  if (l == 0) { wcnt[w] = nev; wbase[w] = ev_base; }
-  if (TM == 3 && l < a.sub_wins) a.subev_cnt[((int64_t)blockIdx.x * kMaxPW + w) * kMaxSubWins + l] = nsub_v;
+  if (l == 0) { wcnt[chk] = nev; wbase[chk] = ev_base; }
+  if (TM == 3 && l < a.sub_wins) a.subev_cnt[((int64_t)blockIdx.x * kMaxCh + chk) * kMaxSubWins + l] = nsub_v;
+  }  // chunks
   MPC_SEG(5);
   __syncthreads();
   MPC_SEG(6);
-  if constexpr (big) parse_epilogue_big(a, n, nbk, r0, wcnt, wbase, nw);
-  else parse_epilogue<TM>(a, n, gb, nbk, r0, hl, bcnt, uni, wcnt, wbase, nw, reinterpret_cast<uint64_t*>(lds),
+  if constexpr (big) parse_epilogue_big(a, n, nbk, r0, wcnt, wbase, nch);
+  else parse_epilogue<TM>(a, n, gb, nbk, r0, hl, bcnt, uni, wcnt, wbase, nch, reinterpret_cast<uint64_t*>(lds),
                           nw * (int)sizeof(WL) / 8);
 #ifdef MPC_STAMPS
   MPC_SEG(7);
@@ -1062,7 +1090,7 @@ constexpr int kSubsWG = 32;  // parse workgroups per K_subs block, at most
 struct SubsArgs {
   const int4* work;    // {sample, window, first parse workgroup, end}
   const int4* pwork;   // parse work table {sample, r0, r1, 0}
-  const int32_t* wave_tab;  // the parse waves' read ranges (kMaxPW + 1 boundaries per workgroup)
+  const int32_t* wave_tab;  // the parse chunks' read ranges (kMaxCh + 1 boundaries per workgroup)
   const int64_t* cs_off; int64_t cs_base;
   const uint16_t* subev; const uint32_t* subev_cnt; int64_t subev_cap;
   const int32_t* n_of; const int32_t* gbase; uint32_t* sub;
@@ -1072,13 +1100,14 @@ __global__ __launch_bounds__(1024) void K_subs(SubsArgs a) {
   __shared__ uint32_t cnt[kSubWin * 2];  // (position, code pair): codes 2h | 2h+1 in the halves
   const int4 wk = a.work[blockIdx.x];
   const int smp = wk.x, win = wk.y, pw0 = wk.z, pw1 = wk.w;
-  const int nreg = (pw1 - pw0) * a.nw_parse, l = lane(), v = threadIdx.x >> 6, nv = blockDim.x >> 6;
+  const int nreg = (pw1 - pw0) * kMaxCh, l = lane(), v = threadIdx.x >> 6, nv = blockDim.x >> 6;
   for (int k = threadIdx.x; k < kSubWin * 2; k += blockDim.x) cnt[k] = 0;
   __syncthreads();
   for (int rg = v; rg < nreg; rg += nv) {
-    const int pw = pw0 + rg / a.nw_parse, ww = rg % a.nw_parse;
-    const int64_t ra = a.wave_tab[(int64_t)pw * (kMaxPW + 1) + ww];  // the parse wave's first read
-    const int c = (int)a.subev_cnt[((int64_t)pw * kMaxPW + ww) * kMaxSubWins + win];
+    const int pw = pw0 + rg / kMaxCh, ww = rg % kMaxCh;  // parse workgroup, chunk
+    if (ww >= a.pwork[pw].w) continue;
+    const int64_t ra = a.wave_tab[(int64_t)pw * (kMaxCh + 1) + ww];  // the chunk's first read
+    const int c = (int)a.subev_cnt[((int64_t)pw * kMaxCh + ww) * kMaxSubWins + win];
     const uint16_t* src = a.subev + (int64_t)win * a.subev_cap + (a.cs_off[ra] - a.cs_base) / 3 + 2 * ra;
     for (int e0 = 0; e0 < c; e0 += 8 * 64) {
       uint32_t ev[8];
@@ -2728,10 +2757,40 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
         p->max_wg_reads = std::max<int64_t>(p->max_wg_reads, y - x);
       }
     }
-    // the waves of every workgroup: contiguous read ranges, again by bytes
-    for (size_t k = 0; k < p->work_parse.size(); k += 4) {
-      cut(p->work_parse[k + 1], p->work_parse[k + 2], p->parse_nw, bnd);
-      for (int w = 0; w <= kMaxPW; ++w) p->work_wave.push_back((int32_t)bnd[(size_t)std::min(w, p->parse_nw)]);
+    // the chunks of every workgroup (its waves take them in turn): nw chunks
+    // with 5/8 of the bytes, then nw with a quarter and nw with the last
+    // eighth, so the last chunks taken are the small ones (measured against 4
+    // groups of 1/2..1/8, 2 groups, equal quarters and one chunk per wave:
+    // DESIGN.md "Parse work split")
+    {
+      constexpr int kGroups = 3;
+      const int nw = p->parse_nw, nch = std::min(kMaxCh, kGroups * nw);
+      std::vector<int64_t> part;
+      for (size_t k = 0; k < p->work_parse.size(); k += 4) {
+        const int64_t a = p->work_parse[k + 1], b = p->work_parse[k + 2];
+        std::vector<int64_t> cb{a};
+        static constexpr double grp[kGroups] = {0.625, 0.25, 0.125};
+        // groups only while the smallest chunks still hold about half a window
+        // (else one chunk per wave: C1's 3 KiB per wave ran 11 % slower cut in three)
+        const int64_t wg_bytes = hco ? hco[b] - hco[a] : (b - a) * (in->cs_bytes / std::max<int64_t>(1, p->N));
+        const int ng = wg_bytes >= 4 * (int64_t)nw * p->parse_win ? kGroups : 1;
+        int64_t lo = a;
+        double acc = 0;
+        for (int g = 0; g < ng && (int)cb.size() - 1 < nch; ++g) {
+          acc += grp[g];
+          int64_t hi = b;
+          if (g < ng - 1) {  // group end: the read where the cumulative byte fraction is reached
+            if (hco) hi = std::lower_bound(hco + a, hco + b + 1, hco[a] + (int64_t)((hco[b] - hco[a]) * acc)) - hco;
+            else hi = a + (int64_t)((b - a) * acc);
+            hi = std::min(std::max(hi, lo), b);
+          }
+          cut(lo, hi, nw, part);
+          for (int c = 1; c <= nw; ++c) cb.push_back(part[(size_t)c]);
+          lo = hi;
+        }
+        p->work_parse[k + 3] = (int32_t)(cb.size() - 1);
+        for (int c = 0; c <= kMaxCh; ++c) p->work_wave.push_back((int32_t)cb[(size_t)std::min<int>(c, (int)cb.size() - 1)]);
+      }
     }
     pw_begin[p->S] = (int)(p->work_parse.size() / 4);
     p->n_parse_wg = pw_begin[p->S];
@@ -2829,7 +2888,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_RUNT, RU * 16, 4);            // per run: inline LEFT bases [bi from the 3' end][code]
   p->subev_cap = p->sub_wins ? in->cs_bytes / 3 + 2 * N + 16 : 0;
   set(mpc_plan::B_SUBEV, p->subev_cap * p->sub_wins, 2);
-  set(mpc_plan::B_SUBCNT, p->sub_wins ? (int64_t)p->n_parse_wg * kMaxPW * kMaxSubWins : 0, 4);
+  set(mpc_plan::B_SUBCNT, p->sub_wins ? (int64_t)p->n_parse_wg * kMaxCh * kMaxSubWins : 0, 4);
   set(mpc_plan::B_WSUB, (int64_t)p->work_sub.size(), 4);
   set(mpc_plan::B_BKCUR, p->tally_mode == 4 ? (int64_t)p->n_parse_wg * p->nbmax : 0, 4);
   set(mpc_plan::B_WWAVE, (int64_t)p->work_wave.size(), 4);
@@ -2859,6 +2918,16 @@ int mpc_plan_get_info(const mpc_plan* p, mpc_plan_info* info) {
   info->workspace_bytes = (int64_t)p->ws_bytes;
   info->pad_ = 0;
   return MPC_OK;
+}
+
+// host copies of the parse work tables (tests / tools): n_wg * 4 int32 records
+// {sample, first read, end read, chunks} and n_wg * (MPC_PARSE_CHUNKS + 1)
+// chunk boundaries; either pointer may be NULL; returns the workgroup count
+int mpc_plan_parse_tables(const mpc_plan* p, int32_t* work, int32_t* chunks) {
+  if (!p) return fail(MPC_E_ARG, "null argument");
+  if (work) std::copy(p->work_parse.begin(), p->work_parse.end(), work);
+  if (chunks) std::copy(p->work_wave.begin(), p->work_wave.end(), chunks);
+  return p->n_parse_wg;
 }
 
 int mpc_plan_workspace_bytes(const mpc_plan* p, size_t* bytes) {

@@ -85,6 +85,11 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise MpcError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() (no CPU fallback)")
+        # libmpc.so links the system ROCm HIP/HSA runtimes while PyTorch carries
+        # its own copies: the process holds two.  Bring PyTorch's up first (the
+        # order every GPU test and the bench run in); loading libmpc.so first
+        # left its first HIP call with "no ROCm-capable device" on the MI355X box.
+        _torch().cuda.is_available()
         L = ctypes.CDLL(LIB_PATH)
         vp, i64, i32, dbl = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double
         L.mpc_version.restype = i32
@@ -138,6 +143,39 @@ def geometry(ref_lens, reads_per_sample, cs_bytes, n_reads_global=None, read_off
         info = PlanInfo()
         _check(L.mpc_plan_get_info(h, ctypes.byref(info)))
         return info.as_dict()
+    finally:
+        L.mpc_plan_destroy(h)
+
+
+PARSE_CHUNKS = 48  # include/mpc.h MPC_PARSE_CHUNKS
+
+
+def parse_split(ref_lens, reads_per_sample, cs_off):
+    """Host-only (no device): the parse work split a Plan over these reads
+    would launch -- (work int32[n_wg, 4] = sample, first read, end read,
+    chunks; chunks int32[n_wg, PARSE_CHUNKS + 1] read boundaries)."""
+    ref_len = np.ascontiguousarray(ref_lens, dtype=np.int64)
+    counts = np.asarray(reads_per_sample, dtype=np.int64)
+    rb = np.ascontiguousarray(np.concatenate([[0], np.cumsum(counts)]), dtype=np.int64)
+    off = np.ascontiguousarray(cs_off, dtype=np.int64)
+    n = int(rb[-1])
+    assert off.shape == (n + 1,)
+    p64 = ctypes.POINTER(ctypes.c_int64)
+    inp = _Input(n_samples=len(ref_len), h_ref_len=ref_len.ctypes.data_as(p64), h_read_begin=rb.ctypes.data_as(p64),
+                 n_reads=n, cs_bytes=int(off[-1]), cs_base=0, read_offset=0, n_reads_global=n, shard=0, n_shards=1,
+                 h_cs_off=off.ctypes.data_as(p64))
+    L = lib()
+    L.mpc_plan_parse_tables.argtypes = [ctypes.c_void_p] * 3
+    h = ctypes.c_void_p()
+    _check(L.mpc_plan_create(ctypes.byref(inp), int((4 * ref_len + 8).sum() + 1024), ctypes.byref(h)))
+    try:
+        n_wg = L.mpc_plan_parse_tables(h, None, None)
+        if n_wg < 0:
+            _check(n_wg)
+        work = np.zeros((n_wg, 4), np.int32)
+        chunks = np.zeros((n_wg, PARSE_CHUNKS + 1), np.int32)
+        _check(L.mpc_plan_parse_tables(h, work.ctypes.data, chunks.ctypes.data) - n_wg)
+        return work, chunks
     finally:
         L.mpc_plan_destroy(h)
 

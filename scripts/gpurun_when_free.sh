@@ -7,7 +7,7 @@ T=$1; LOG=$2; CMD=$3
 for attempt in $(seq 1 12); do
   /usr/local/graft/bin/gpurun --timeout "$T" -- "$CMD" > "$LOG" 2>&1
   rc=$?
-  if grep -q "status=transient" "$LOG" && grep -q "run 0.0s" "$LOG"; then
+  if grep -q "status=transient" "$LOG" && grep -qE "run (0.0s|Nones)" "$LOG"; then
     echo "attempt $attempt: no box free, waiting" >> "$LOG.attempts"
     sleep 150
     continue

@@ -4,6 +4,7 @@ import ctypes
 import os
 import re
 
+import numpy as np
 import pytest
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -93,3 +94,39 @@ def test_planner_reference_limit(pkg):
     assert top["tally_mode"] == 4
     with pytest.raises(pkg.engine.MpcError):
         g([(1 << 20) - 1], [12], (1 << 20) * 3)
+
+
+@pytest.mark.parametrize("shape", [
+    ([2686, 2686], [100_000, 100_000]),  # C2
+    ([10_000], [200_000]),               # C3 shape, fewer reads
+    ([30_000] * 6, [10_000] * 6),        # C5 shape, fewer runs
+    ([500, 40_000], [37, 3]),            # ragged: fewer reads than waves
+])
+def test_parse_split(pkg, shape):
+    """Host-only: the parse work split (mpc_plan_parse_tables).  Workgroups
+    cover every sample's reads once, in order; each workgroup's chunks are a
+    contiguous, ordered cut of its reads (at most 3 per wave, include/mpc.h
+    MPC_PARSE_CHUNKS bound); the first group of chunks carries about 5/8 of
+    the workgroup's cs bytes and the last ones the smallest share."""
+    e = pkg.engine
+    ref_lens, counts = shape
+    rng = np.random.default_rng(7)
+    lens = rng.integers(20, 4000, size=sum(counts)) * rng.choice([1, 1, 1, 9], size=sum(counts))
+    off = np.concatenate([[0], np.cumsum(lens)])
+    work, ch = e.parse_split(ref_lens, counts, off)
+    info = e.geometry(ref_lens, counts, int(off[-1]))
+    nw = info["parse_waves"]
+    rb = np.concatenate([[0], np.cumsum(counts)])
+    for s in range(len(counts)):
+        w = work[work[:, 0] == s]
+        assert w[0, 1] == rb[s] and w[-1, 2] == rb[s + 1]
+        assert (w[1:, 1] == w[:-1, 2]).all() and (w[:, 2] > w[:, 1]).all()
+    for (s, a, b, nch), c in zip(work, ch):
+        assert 1 <= nch <= min(3 * nw, e.PARSE_CHUNKS)
+        cb = c[: nch + 1]
+        assert cb[0] == a and cb[-1] == b and (np.diff(cb) >= 0).all()
+        assert (c[nch:] == b).all()  # padding repeats the end
+        if b - a >= 8 * nw and nch == 3 * nw:
+            tot = off[b] - off[a]
+            first = off[cb[nw]] - off[a]
+            assert 0.45 * tot <= first <= 0.8 * tot, (first, tot)

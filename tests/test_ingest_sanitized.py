@@ -37,9 +37,13 @@ def asan_bin():
     os.makedirs(os.path.dirname(BIN), exist_ok=True)
     src = [os.path.join(REPO, "minion-plasmid-consensus_amd", "csrc", f) for f in
            ("ingest.cpp", "writers.cpp", "pseudopair.cpp")] + [os.path.join(REPO, "tests", "native", "ingest_driver.cpp")]
+    # build under a per-process name, then rename: pytest-xdist workers each
+    # build it, and one must never exec a file another is still writing
+    tmp = "%s.%d" % (BIN, os.getpid())
     subprocess.run(["g++", "-std=c++17", "-O1", "-g", "-fno-omit-frame-pointer", "-fsanitize=address,undefined",
-                    "-fno-sanitize-recover=all", "-pthread", "-I", os.path.join(REPO, "include"), "-o", BIN] + src,
+                    "-fno-sanitize-recover=all", "-pthread", "-I", os.path.join(REPO, "include"), "-o", tmp] + src,
                    check=True)
+    os.replace(tmp, BIN)
     return BIN
 
 

@@ -20,6 +20,7 @@
 #include "mpc_ingest.h"
 
 #include <fcntl.h>
+#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -74,6 +75,21 @@ inline sv rstrip(sv s) {
   return s.substr(0, e);
 }
 inline char upper(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 32) : c; }
+
+// Threads to use by default: OMP_NUM_THREADS when set (the GPU pool sets it to
+// the job's CPU share), else the CPUs this process may run on.  Not
+// hardware_concurrency(): that counts the whole machine, and a shared box
+// gives a job a fraction of it.
+int host_threads() {
+  if (const char* e = getenv("OMP_NUM_THREADS")) {
+    const int v = atoi(e);
+    if (v > 0) return v;
+  }
+  cpu_set_t cs;
+  if (sched_getaffinity(0, sizeof(cs), &cs) == 0 && CPU_COUNT(&cs) > 0) return CPU_COUNT(&cs);
+  const unsigned hw = std::thread::hardware_concurrency();
+  return hw ? (int)hw : 4;
+}
 
 template <class F>
 void parallel(int T, F f) {
@@ -222,8 +238,7 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
     if (code != MPC_INGEST_OK) mpc_ingest_free(out);
     return code;
   };
-  unsigned hw = std::thread::hardware_concurrency();
-  const int T = std::max(1, std::min(n_threads > 0 ? n_threads : (int)(hw ? hw : 4), 64));
+  const int T = std::max(1, std::min(n_threads > 0 ? n_threads : host_threads(), 64));
   Mapped fr, fp, fa;
   if (!fr.open(ref_path)) return finish(MPC_INGEST_ERROR, std::string("cannot open ") + ref_path);
   if (!fp.open(paf_path)) return finish(MPC_INGEST_ERROR, std::string("cannot open ") + paf_path);
@@ -267,15 +282,42 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
   int64_t n_lines = 0;
   size_t total = 0;
   for (int k = 0; k < T; ++k) { n_lines += nlines[k]; total += recs[k].size(); }
-  std::vector<PafRec> keep;
-  keep.reserve(total);
-  std::unordered_map<sv, int64_t> by_name;
-  by_name.reserve(total * 2 + 16);
-  for (int k = 0; k < T; ++k)
-    for (const PafRec& r : recs[k])
-      if (by_name.emplace(r.name, (int64_t)keep.size()).second) keep.push_back(r);  // first line wins (:237-243)
+  // first line per name wins (:237-243).  Names are sharded by hash: thread s
+  // walks every record in file order and keeps the names of its shard in its
+  // own map, so the first occurrence is found without a serial pass over a
+  // million-entry map; the kept records are then compacted in file order.
+  std::vector<PafRec> all;
+  all.reserve(total);
+  for (int k = 0; k < T; ++k) all.insert(all.end(), recs[k].begin(), recs[k].end());
   recs.clear();
+  const int64_t NA = (int64_t)all.size();
+  std::vector<uint32_t> hsh((size_t)NA);
+  std::vector<uint8_t> first((size_t)NA, 0);
+  parallel(T, [&](int k) {
+    const std::hash<sv> h;
+    for (int64_t i = NA * k / T; i < NA * (k + 1) / T; ++i) hsh[(size_t)i] = (uint32_t)h(all[(size_t)i].name);
+  });
+  std::vector<std::unordered_map<sv, int64_t>> shard((size_t)T);  // name -> index in all, then in keep
+  parallel(T, [&](int k) {
+    auto& m = shard[(size_t)k];
+    m.reserve((size_t)(2 * NA / T + 16));
+    for (int64_t i = 0; i < NA; ++i)
+      if (hsh[(size_t)i] % (uint32_t)T == (uint32_t)k && m.emplace(all[(size_t)i].name, i).second) first[(size_t)i] = 1;
+  });
+  std::vector<int64_t> kidx((size_t)NA, -1);
+  std::vector<PafRec> keep;
+  keep.reserve((size_t)NA);
+  for (int64_t i = 0; i < NA; ++i)
+    if (first[(size_t)i]) { kidx[(size_t)i] = (int64_t)keep.size(); keep.push_back(all[(size_t)i]); }
+  parallel(T, [&](int k) {
+    for (auto& kv : shard[(size_t)k]) kv.second = kidx[(size_t)kv.second];
+  });
   const int64_t N = (int64_t)keep.size();
+  auto lookup = [&](sv name) -> int64_t {  // record of a read name, -1: not in the PAF
+    const auto& m = shard[(size_t)((uint32_t)std::hash<sv>()(name) % (uint32_t)T)];
+    auto it = m.find(name);
+    return it == m.end() ? -1 : it->second;
+  };
 
   // ---- Step 3: reads FASTA (:253-277), chunks of records in parallel ----
   std::vector<Flank> flanks(N);
@@ -291,38 +333,74 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
   };
   parallel(T, [&](int k) {
     const size_t a = k == 0 ? 0 : rec_start(fa.n * k / T), b = k == T - 1 ? fa.n : rec_start(fa.n * (k + 1) / T);
-    std::string seq, rc;
+    // A record's sequence is never materialized: its lines stay in the mapping as
+    // (start, rstripped length) spans, and only the flank bytes are copied out
+    // (a 10 kb read has ~80 flank bytes).  seq = "".join(line.rstrip().upper())
+    // (:270), so seq[i] is upper() of the span byte at position i.
+    std::vector<sv> spans;
+    std::vector<int64_t> span_end;  // cumulative rstripped length after each span
     int64_t cur = -1;        // record of the current name, -1: not in the PAF (or before the first header)
     size_t cur_pos = 0;
+    // copy seq[i0, i1) (upper-cased) to dst, forward
+    auto copy_fwd = [&](int64_t i0, int64_t i1, char* dst) {
+      size_t j = std::upper_bound(span_end.begin(), span_end.end(), i0) - span_end.begin();
+      for (int64_t i = i0; i < i1; ++j) {
+        const int64_t s0 = span_end[j] - (int64_t)spans[j].size();
+        const int64_t e = std::min(i1, span_end[j]);
+        for (; i < e; ++i) *dst++ = upper(spans[j][(size_t)(i - s0)]);
+      }
+    };
     auto done = [&]() {      // :259-265 for the record just read
       if (cur < 0) return;
       const PafRec& r = keep[cur];
-      const std::string* s = &seq;
-      if (r.minus) {  // "".join([BASE_COMPLIMENT[x.upper()] for x in seq[::-1]]) (:263)
-        rc.resize(seq.size());
-        for (size_t i = 0; i < seq.size(); ++i) {
-          const char c = seq[seq.size() - 1 - i];
-          char o;
-          switch (c) {
-            case 'A': o = 'T'; break; case 'T': o = 'A'; break; case 'G': o = 'C'; break;
-            case 'C': o = 'G'; break; case 'N': o = 'N'; break;
-            default:
-              ffails[k].set(MPC_INGEST_ERROR, cur_pos, "KeyError: '" + std::string(1, c) + "' (reverse complement of read " +
-                                                           std::string(r.name.substr(0, 80)) + ")");
-              return;
+      const int64_t L = span_end.empty() ? 0 : span_end.back();
+      if (r.minus) {
+        // "".join([BASE_COMPLIMENT[x.upper()] for x in seq[::-1]]) (:263): a KeyError
+        // for any byte of the WHOLE sequence outside ACGTN (after upper(); for
+        // ASCII, (c & 0xDF) is upper() on letters and maps no other byte onto
+        // A, C, G, T, N).  The first offending byte in seq[::-1] order is reported.
+        bool bad = false;
+        for (const sv& s : spans) {
+          unsigned ok = 1;
+          for (char ch : s) {
+            const unsigned u = (unsigned char)ch & 0xDFu;
+            ok &= (unsigned)((u == 'A') | (u == 'C') | (u == 'G') | (u == 'T') | (u == 'N'));
           }
-          rc[i] = o;
+          bad |= !ok;
         }
-        s = &rc;
+        if (bad) {
+          char c = '?';
+          for (auto it = spans.rbegin(); it != spans.rend() && c == '?'; ++it)
+            for (size_t i = it->size(); i-- > 0;) {
+              const unsigned u = (unsigned char)(*it)[i] & 0xDFu;
+              if (!(u == 'A' || u == 'C' || u == 'G' || u == 'T' || u == 'N')) { c = upper((*it)[i]); break; }
+            }
+          ffails[k].set(MPC_INGEST_ERROR, cur_pos, "KeyError: '" + std::string(1, c) + "' (reverse complement of read " +
+                                                       std::string(r.name.substr(0, 80)) + ")");
+          return;
+        }
       }
-      const int64_t L = (int64_t)s->size();
       const int64_t u = py_cut(L, r.qs), d = py_cut(L, r.qe);
+      std::string up((size_t)u, '\0'), down((size_t)(L - d), '\0');
+      if (!r.minus) {
+        copy_fwd(0, u, &up[0]);
+        copy_fwd(d, L, &down[0]);
+      } else {  // rc[i] = comp(seq[L-1-i]): rc[:u] from seq[L-u, L), rc[d:] from seq[0, L-d), both reversed
+        auto comp_rev = [](std::string& s) {
+          std::reverse(s.begin(), s.end());
+          for (char& c : s) c = c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'G' ? 'C' : c == 'C' ? 'G' : 'N';
+        };
+        copy_fwd(L - u, L, &up[0]);
+        comp_rev(up);
+        copy_fwd(0, L - d, &down[0]);
+        comp_rev(down);
+      }
       std::lock_guard<std::mutex> g(locks[cur & 63]);
       Flank& fl = flanks[cur];
       if (fl.pos == SIZE_MAX || cur_pos > fl.pos) {  // a duplicate name: the last record wins
         fl.pos = cur_pos;
-        fl.up.assign(s->data(), (size_t)u);
-        fl.down.assign(s->data() + d, (size_t)(L - d));
+        fl.up = std::move(up);
+        fl.down = std::move(down);
       }
     };
     for (size_t x = a; x < b;) {
@@ -332,12 +410,16 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
       if (!line.empty() && line[0] == '>') {
         done();
         const sv name = rstrip(line).substr(1);  // whole header line (:267); "" is never processed (:260)
-        auto it = name.empty() ? by_name.end() : by_name.find(name);
-        cur = it == by_name.end() ? -1 : it->second;
+        cur = name.empty() ? -1 : lookup(name);
         cur_pos = x;
-        seq.clear();
+        spans.clear();
+        span_end.clear();
       } else if (cur >= 0) {
-        for (char c : rstrip(line)) seq.push_back(upper(c));  // :270
+        const sv s = rstrip(line);  // :270
+        if (!s.empty()) {
+          spans.push_back(s);
+          span_end.push_back((span_end.empty() ? 0 : span_end.back()) + (int64_t)s.size());
+        }
       }
       x = e + 1;
     }
@@ -365,15 +447,23 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
   out->down_off = (int64_t*)alloc(8 * (N + 1));
   out->tstart = (int64_t*)alloc(8 * N); out->aligned = (int64_t*)alloc(8 * N);
   size_t oc = 0, ou = 0, od = 0;
-  for (int64_t i = 0; i < N; ++i) {
+  for (int64_t i = 0; i < N; ++i) {  // offsets (serial prefix), then the copies by read ranges on all threads
     out->cs_off[i] = (int64_t)oc; out->up_off[i] = (int64_t)ou; out->down_off[i] = (int64_t)od;
-    memcpy(out->cs + oc, keep[i].cs.data(), keep[i].cs.size()); oc += keep[i].cs.size();
-    memcpy(out->up + ou, flanks[i].up.data(), flanks[i].up.size()); ou += flanks[i].up.size();
-    memcpy(out->down + od, flanks[i].down.data(), flanks[i].down.size()); od += flanks[i].down.size();
+    oc += keep[i].cs.size(); ou += flanks[i].up.size(); od += flanks[i].down.size();
     out->tstart[i] = keep[i].ts;
     out->aligned[i] = keep[i].qe - keep[i].qs;
   }
   out->cs_off[N] = (int64_t)oc; out->up_off[N] = (int64_t)ou; out->down_off[N] = (int64_t)od;
+  parallel(T, [&](int k) {
+    // read range of thread k: equal shares of the cs bytes (the bulk of the copy)
+    auto at = [&](size_t x) { return (int64_t)(std::lower_bound(out->cs_off, out->cs_off + N, (int64_t)x) - out->cs_off); };
+    const int64_t i0 = at(oc * k / T), i1 = k == T - 1 ? N : at(oc * (k + 1) / T);
+    for (int64_t i = i0; i < i1; ++i) {
+      memcpy(out->cs + out->cs_off[i], keep[i].cs.data(), keep[i].cs.size());
+      memcpy(out->up + out->up_off[i], flanks[i].up.data(), flanks[i].up.size());
+      memcpy(out->down + out->down_off[i], flanks[i].down.data(), flanks[i].down.size());
+    }
+  });
   out->n_reads = N;
   out->n_alignments = n_lines;
   return finish(MPC_INGEST_OK, "");

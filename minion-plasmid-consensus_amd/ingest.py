@@ -181,33 +181,51 @@ def pack_sample_native(ref_path, paf_path, reads_path, n_threads=0):
     L = _native()
     if L is None:
         return None
-    o = _IngestOut()
+    own = _IngestBuffers(L)
+    o = own.out
     enc = lambda p: os.fsencode(p)
     L.mpc_ingest(enc(ref_path), enc(paf_path), enc(reads_path), int(n_threads), ctypes.byref(o))
-    try:
-        if o.status == INGEST_FALLBACK:
-            return None
-        if o.status != INGEST_OK:
-            raise IngestError(o.message.decode(errors="replace"))
-        n = o.n_reads
+    if o.status == INGEST_FALLBACK:
+        return None
+    if o.status != INGEST_OK:
+        raise IngestError(o.message.decode(errors="replace"))
+    n = o.n_reads
+    # zero-copy: the arrays are views of the library's buffers (a GB of cs at
+    # C3), freed once the last view is gone
+    cs_off = own.view(o.cs_off, n + 1, ctypes.c_int64)
+    up_off = own.view(o.up_off, n + 1, ctypes.c_int64)
+    dn_off = own.view(o.down_off, n + 1, ctypes.c_int64)
+    return dict(
+        ref=own.view(o.ref, o.ref_len, ctypes.c_uint8),
+        cs=own.view(o.cs, int(cs_off[-1]), ctypes.c_uint8), cs_off=cs_off,
+        tstart=own.view(o.tstart, n, ctypes.c_int64),
+        up=own.view(o.up, int(up_off[-1]), ctypes.c_uint8), up_off=up_off,
+        down=own.view(o.down, int(dn_off[-1]), ctypes.c_uint8), down_off=dn_off,
+        aligned=own.view(o.aligned, n, ctypes.c_int64),
+        n_alignments=int(o.n_alignments),
+    )
 
-        def arr(p, k, dt):
-            return np.ctypeslib.as_array(p, shape=(k,)).astype(dt, copy=True) if k else np.zeros(0, dtype=dt)
 
-        cs_off = arr(o.cs_off, n + 1, np.int64)
-        up_off = arr(o.up_off, n + 1, np.int64)
-        dn_off = arr(o.down_off, n + 1, np.int64)
-        return dict(
-            ref=arr(o.ref, o.ref_len, np.uint8),
-            cs=arr(o.cs, int(cs_off[-1]), np.uint8), cs_off=cs_off,
-            tstart=arr(o.tstart, n, np.int64),
-            up=arr(o.up, int(up_off[-1]), np.uint8), up_off=up_off,
-            down=arr(o.down, int(dn_off[-1]), np.uint8), down_off=dn_off,
-            aligned=arr(o.aligned, n, np.int64),
-            n_alignments=int(o.n_alignments),
-        )
-    finally:
-        L.mpc_ingest_free(ctypes.byref(o))
+class _IngestBuffers:
+    """Owner of one mpc_ingest result: numpy views of its buffers keep it alive
+    (through their ctypes base), and it frees them when the last view goes."""
+
+    def __init__(self, lib):
+        self.lib = lib
+        self.out = _IngestOut()
+
+    def view(self, ptr, k, ct):
+        if k <= 0:
+            return np.zeros(0, dtype=ct)
+        buf = (ct * int(k)).from_address(ctypes.addressof(ptr.contents))
+        buf._owner = self
+        return np.frombuffer(buf, dtype=ct)
+
+    def __del__(self):
+        lib = getattr(self, "lib", None)
+        if lib is not None:
+            lib.mpc_ingest_free(ctypes.byref(self.out))
+            self.lib = None
 
 
 def pack_sample(ref_path, paf_path, reads_path, native=True):

@@ -95,6 +95,10 @@ EDGE = {
     "slicing": (">r\nACGTACGTAC\n",
                 paf_line("s", 30, 25, 35, "+", 0, ":10") + paf_line("t", 5, 1, 40, "-", 0, ":10"),
                 ">s\nACGTACGTACGT\n>t\nACGTACGTACGTAAA\n"),
+    # flank cuts across line boundaries, blank and whitespace-only lines inside records, lower-case n
+    "spans": (">r\nACGTACGTACGT\n",
+              paf_line("p", 17, 3, 14, "+", 0, ":11") + paf_line("q", 17, 2, 15, "-", 0, ":13"),
+              ">p\nac\n\ngTa  \n \nCGTAcgtnacGT\n>q\nAC\ngtA\n\nnCGTACg\t\ntacg\n"),
     "empty_paf": (">r\nACGT\n", "", ">a\nACGT\n"),
     "no_newline_at_end": (">r\nACGTACGTAC", paf_line("a", 10, 0, 10, "+", 0, ":10").rstrip("\n"), ">a\nACGTACGTAC"),
     "cs_first_field_wins": (">r\nACGTACGTAC\n", paf_line("a", 10, 0, 10, "+", 0, ":10", extra="cs:Z::3"),
@@ -104,6 +108,7 @@ EDGE = {
 ERRORS = {
     "missing_read": (">r\nACGT\n", paf_line("a", 4, 0, 4, "+", 0, ":4"), ">b\nACGT\n"),
     "minus_bad_char": (">r\nACGT\n", paf_line("a", 4, 0, 4, "-", 0, ":4"), ">a\nACXT\n"),
+    "minus_bad_lower": (">r\nACGT\n", paf_line("a", 6, 0, 6, "-", 0, ":4"), ">a\nAC\ngt\nAx\n"),
     "no_cs": (">r\nACGT\n", "a\t4\t0\t4\t+\tref\t4\t0\t4\t4\t4\t60\n", ">a\nACGT\n"),
     "short_line": (">r\nACGT\n", "a\t4\t0\n", ">a\nACGT\n"),
     "bad_int": (">r\nACGT\n", paf_line("a", 4, 0, 4, "+", 0, ":4").replace("\t4\t0\t4\t", "\t4\tx\t4\t", 1), ">a\nACGT\n"),

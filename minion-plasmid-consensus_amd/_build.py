@@ -29,7 +29,7 @@ def _stale(target, sources):
 
 def build_synth(force=False):
     src = os.path.join(CSRC, "synth.cpp")
-    if force or _stale(LIBSYNTH, [src]):
+    if force or _stale(LIBSYNTH, [src, os.path.join(CSRC, "host_threads.h")]):
         subprocess.run(["g++", "-O2", "-std=c++17", "-fPIC", "-shared", "-pthread", "-o", LIBSYNTH, src], check=True)
     return LIBSYNTH
 
@@ -41,7 +41,7 @@ def ensure_synth():
 def build_ingest(force=False):
     srcs = [os.path.join(CSRC, f) for f in ("ingest.cpp", "writers.cpp", "pseudopair.cpp")]
     hdr = os.path.join(INCLUDE, "mpc_ingest.h")
-    if force or _stale(LIBINGEST, srcs + [hdr]):
+    if force or _stale(LIBINGEST, srcs + [hdr, os.path.join(CSRC, "host_threads.h")]):
         subprocess.run(["g++", "-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-I", INCLUDE, "-o", LIBINGEST] + srcs,
                        check=True)
     return LIBINGEST

@@ -18,9 +18,9 @@
 // all cores: PAF lines and FASTA records are independent, only the PAF dedup
 // (file order) is sequential.
 #include "mpc_ingest.h"
+#include "host_threads.h"
 
 #include <fcntl.h>
-#include <sched.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
@@ -76,20 +76,7 @@ inline sv rstrip(sv s) {
 }
 inline char upper(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 32) : c; }
 
-// Threads to use by default: OMP_NUM_THREADS when set (the GPU pool sets it to
-// the job's CPU share), else the CPUs this process may run on.  Not
-// hardware_concurrency(): that counts the whole machine, and a shared box
-// gives a job a fraction of it.
-int host_threads() {
-  if (const char* e = getenv("OMP_NUM_THREADS")) {
-    const int v = atoi(e);
-    if (v > 0) return v;
-  }
-  cpu_set_t cs;
-  if (sched_getaffinity(0, sizeof(cs), &cs) == 0 && CPU_COUNT(&cs) > 0) return CPU_COUNT(&cs);
-  const unsigned hw = std::thread::hardware_concurrency();
-  return hw ? (int)hw : 4;
-}
+using mpc_host::host_threads;
 
 template <class F>
 void parallel(int T, F f) {

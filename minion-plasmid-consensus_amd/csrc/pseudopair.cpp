@@ -16,6 +16,7 @@
 // form only Python's int() accepts, bytes >= 0x80, '\r' (universal newlines)
 // -- are declined (status MPC_INGEST_FALLBACK): the caller uses the Python
 // restatement.
+#include "host_threads.h"
 #include <fcntl.h>
 #include <sys/mman.h>
 #include <sys/stat.h>
@@ -119,7 +120,7 @@ int mpc_pseudopair(const char* paf_path, int64_t min_align_length, int has_min, 
   }
   const size_t L = starts.size();
   std::vector<Rec> recs(L);
-  int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  int nt = n_threads > 0 ? n_threads : mpc_host::host_threads();
   nt = (int)std::max<size_t>(1, std::min<size_t>((size_t)nt, L / 4096 + 1));
   std::vector<uint8_t> odd((size_t)nt, 0);  // bytes the parser declines
   auto work = [&](int t) {

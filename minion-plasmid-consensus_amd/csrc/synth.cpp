@@ -12,6 +12,7 @@
 // reference script (golden fixtures), the C oracle and the HIP path.
 //
 // The generator is test/bench infrastructure, not part of the hot path.
+#include "host_threads.h"
 #include <cmath>
 #include <cstdint>
 #include <cstdio>
@@ -235,7 +236,7 @@ void* mpc_synth_new(const mpc_synth_params* pp) {
   h->p.read_begin = R0;
   h->p.read_end = R1;
   const int64_t N = R1 - R0;
-  int nt = p.n_threads > 0 ? p.n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  int nt = p.n_threads > 0 ? p.n_threads : mpc_host::host_threads();
   nt = std::min(nt, 16);  // the GPU box's CPU share
   nt = (int)std::min<int64_t>(nt, std::max<int64_t>(1, N / 256));
   struct Part {

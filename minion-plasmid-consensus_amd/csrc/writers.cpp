@@ -15,6 +15,7 @@
 // and written one after the other, as the reference does (:447, :453, :460), so
 // an open/write failure on a later file leaves the earlier ones written, exactly
 // like the reference (Snakemake removes the outputs of a failed job).
+#include "host_threads.h"
 #include <charconv>
 #include <cmath>
 #include <cstdint>
@@ -122,7 +123,7 @@ int mpc_py_float_repr(double x, char* out, int out_len) {
 int mpc_write_calls(const uint32_t* calls, int64_t n_calls, const char* consensus_path, const char* chromat_path,
                     const char* accuracies_path, int n_threads, char* msg, int msg_len) {
   if (n_calls < 0 || (n_calls > 0 && !calls)) { std::snprintf(msg, (size_t)msg_len, "bad arguments"); return -1; }
-  int nt = n_threads > 0 ? n_threads : (int)std::max(1u, std::thread::hardware_concurrency());
+  int nt = n_threads > 0 ? n_threads : mpc_host::host_threads();
   nt = (int)std::min<int64_t>(nt, std::max<int64_t>(1, n_calls / 8192));
   std::string cons;
   cons.reserve((size_t)n_calls + 16);

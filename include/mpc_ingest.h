@@ -84,6 +84,12 @@ int mpc_pseudopair(const char* paf_path, int64_t min_align_length, int has_min, 
 /* n_threads <= 0: all hardware threads.  Returns out->status. */
 int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_path, int n_threads,
                mpc_ingest_out* out);
+/* Several (assembly, PAF) jobs against ONE reads FASTA (sense + antisense of a
+ * sample, Snakefile:401-423): the reads file is scanned once for all of them.
+ * outs[j] is exactly what mpc_ingest(ref_paths[j], paf_paths[j], reads_path)
+ * returns (each has its own status); returns outs[0].status. */
+int mpc_ingest_multi(int n_jobs, const char* const* ref_paths, const char* const* paf_paths, const char* reads_path,
+                     int n_threads, mpc_ingest_out* outs);
 void mpc_ingest_free(mpc_ingest_out* out);
 
 #ifdef __cplusplus

@@ -202,50 +202,40 @@ struct Flank {
   std::string up, down;
 };
 
-}  // namespace
 
-extern "C" {
-
-int mpc_ingest_version(void) { return 2; }  // 2: + mpc_write_calls, mpc_py_float_repr, pseudopair
-
-void mpc_ingest_free(mpc_ingest_out* o) {
-  if (!o) return;
-  free(o->ref); free(o->cs); free(o->cs_off); free(o->tstart); free(o->up); free(o->up_off);
-  free(o->down); free(o->down_off); free(o->aligned);
-  o->ref = o->cs = o->up = o->down = nullptr;
-  o->cs_off = o->tstart = o->up_off = o->down_off = o->aligned = nullptr;
-}
-
-int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_path, int n_threads,
-               mpc_ingest_out* out) {
-  memset(out, 0, sizeof(*out));
-  auto finish = [&](int code, const std::string& msg) {
-    out->status = code;
-    snprintf(out->message, sizeof(out->message), "%s", msg.c_str());
-    if (code != MPC_INGEST_OK) mpc_ingest_free(out);
-    return code;
-  };
-  const int T = std::max(1, std::min(n_threads > 0 ? n_threads : host_threads(), 64));
-  Mapped fr, fp, fa;
-  if (!fr.open(ref_path)) return finish(MPC_INGEST_ERROR, std::string("cannot open ") + ref_path);
-  if (!fp.open(paf_path)) return finish(MPC_INGEST_ERROR, std::string("cannot open ") + paf_path);
-  if (!fa.open(reads_path)) return finish(MPC_INGEST_ERROR, std::string("cannot open ") + reads_path);
-  if (needs_python(fr, T) || needs_python(fp, T) || needs_python(fa, T))
-    return finish(MPC_INGEST_FALLBACK, "non-ASCII byte or carriage return: Python text-mode semantics");
-
-  // ---- Step 1: reference (:161-184) ----
+// One (assembly, PAF) job of a launch.  Several jobs may share ONE reads FASTA
+// (the sense and antisense consensus jobs of a sample, Snakefile:401-423): it
+// is then scanned once for all of them (mpc_ingest_multi).
+struct Job {
+  Mapped fr, fp;
   std::string ref;
-  ref.reserve(fr.n);
-  for (size_t a = 0; a < fr.n;) {
-    const char* nl = static_cast<const char*>(memchr(fr.p + a, '\n', fr.n - a));
-    const size_t e = nl ? (size_t)(nl - fr.p) : fr.n;
-    const sv line(fr.p + a, e - a);
+  std::vector<PafRec> keep;                              // first line per read name, file order
+  std::vector<std::unordered_map<sv, int64_t>> shard;    // name -> index in keep, sharded by hash
+  std::vector<Flank> flanks;
+  int64_t n_lines = 0;
+  Fail fail;
+  bool live = true;  // Steps 1-2 passed: take part in Step 3
+  int64_t lookup(sv name) const {  // record of a read name, -1: not in this PAF
+    const auto& m = shard[(size_t)((uint32_t)std::hash<sv>()(name) % (uint32_t)shard.size())];
+    auto it = m.find(name);
+    return it == m.end() ? -1 : it->second;
+  }
+};
+
+// Steps 1-2 of one job (the files are open and ASCII-checked)
+void job_ref_paf(Job& J, int T) {
+  // ---- Step 1: reference (:161-184) ----
+  J.ref.reserve(J.fr.n);
+  for (size_t a = 0; a < J.fr.n;) {
+    const char* nl = static_cast<const char*>(memchr(J.fr.p + a, '\n', J.fr.n - a));
+    const size_t e = nl ? (size_t)(nl - J.fr.p) : J.fr.n;
+    const sv line(J.fr.p + a, e - a);
     if (line.empty() || line[0] != '>')
-      for (char c : rstrip(line)) ref.push_back(upper(c));
+      for (char c : rstrip(line)) J.ref.push_back(upper(c));
     a = e + 1;
   }
-
   // ---- Step 2: PAF (:192-245), chunks of lines in parallel, dedup in file order ----
+  const Mapped& fp = J.fp;
   std::vector<std::vector<PafRec>> recs(T);
   std::vector<Fail> fails(T);
   std::vector<int64_t> nlines(T, 0);
@@ -263,12 +253,10 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
       x = e + 1;
     }
   });
-  Fail fail;
-  for (auto& f : fails) fail.merge(f);
-  if (fail.code != MPC_INGEST_OK) return finish(fail.code, fail.msg);
-  int64_t n_lines = 0;
+  for (auto& f : fails) J.fail.merge(f);
+  if (J.fail.code != MPC_INGEST_OK) { J.live = false; return; }
   size_t total = 0;
-  for (int k = 0; k < T; ++k) { n_lines += nlines[k]; total += recs[k].size(); }
+  for (int k = 0; k < T; ++k) { J.n_lines += nlines[k]; total += recs[k].size(); }
   // first line per name wins (:237-243).  Names are sharded by hash: thread s
   // walks every record in file order and keeps the names of its shard in its
   // own map, so the first occurrence is found without a serial pass over a
@@ -284,32 +272,33 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
     const std::hash<sv> h;
     for (int64_t i = NA * k / T; i < NA * (k + 1) / T; ++i) hsh[(size_t)i] = (uint32_t)h(all[(size_t)i].name);
   });
-  std::vector<std::unordered_map<sv, int64_t>> shard((size_t)T);  // name -> index in all, then in keep
+  J.shard.resize((size_t)T);
   parallel(T, [&](int k) {
-    auto& m = shard[(size_t)k];
+    auto& m = J.shard[(size_t)k];
     m.reserve((size_t)(2 * NA / T + 16));
     for (int64_t i = 0; i < NA; ++i)
       if (hsh[(size_t)i] % (uint32_t)T == (uint32_t)k && m.emplace(all[(size_t)i].name, i).second) first[(size_t)i] = 1;
   });
   std::vector<int64_t> kidx((size_t)NA, -1);
-  std::vector<PafRec> keep;
-  keep.reserve((size_t)NA);
+  J.keep.reserve((size_t)NA);
   for (int64_t i = 0; i < NA; ++i)
-    if (first[(size_t)i]) { kidx[(size_t)i] = (int64_t)keep.size(); keep.push_back(all[(size_t)i]); }
+    if (first[(size_t)i]) { kidx[(size_t)i] = (int64_t)J.keep.size(); J.keep.push_back(all[(size_t)i]); }
   parallel(T, [&](int k) {
-    for (auto& kv : shard[(size_t)k]) kv.second = kidx[(size_t)kv.second];
+    for (auto& kv : J.shard[(size_t)k]) kv.second = kidx[(size_t)kv.second];
   });
-  const int64_t N = (int64_t)keep.size();
-  auto lookup = [&](sv name) -> int64_t {  // record of a read name, -1: not in the PAF
-    const auto& m = shard[(size_t)((uint32_t)std::hash<sv>()(name) % (uint32_t)T)];
-    auto it = m.find(name);
-    return it == m.end() ? -1 : it->second;
-  };
+  J.flanks.resize(J.keep.size());
+}
 
-  // ---- Step 3: reads FASTA (:253-277), chunks of records in parallel ----
-  std::vector<Flank> flanks(N);
+// Step 3 (:253-277) for every live job, ONE pass over the reads FASTA: chunks of
+// records in parallel.  A record's sequence is never materialized: its lines
+// stay in the mapping as (start, rstripped length) spans and only the flank
+// bytes are copied out (a 10 kb read has ~80 flank bytes).
+// seq = "".join(line.rstrip().upper()) (:270), so seq[i] is upper() of the span
+// byte at position i.
+void jobs_fasta(std::vector<Job>& jobs, const Mapped& fa, int T) {
+  const int nj = (int)jobs.size();
   std::mutex locks[64];
-  std::vector<Fail> ffails(T);
+  std::vector<std::vector<Fail>> ffails((size_t)nj, std::vector<Fail>((size_t)T));
   auto rec_start = [&](size_t x) {  // first header line ('>' at a line start) at or after x
     size_t y = line_start_at_or_after(fa, x);
     while (y < fa.n && fa.p[y] != '>') {
@@ -320,14 +309,13 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
   };
   parallel(T, [&](int k) {
     const size_t a = k == 0 ? 0 : rec_start(fa.n * k / T), b = k == T - 1 ? fa.n : rec_start(fa.n * (k + 1) / T);
-    // A record's sequence is never materialized: its lines stay in the mapping as
-    // (start, rstripped length) spans, and only the flank bytes are copied out
-    // (a 10 kb read has ~80 flank bytes).  seq = "".join(line.rstrip().upper())
-    // (:270), so seq[i] is upper() of the span byte at position i.
     std::vector<sv> spans;
-    std::vector<int64_t> span_end;  // cumulative rstripped length after each span
-    int64_t cur = -1;        // record of the current name, -1: not in the PAF (or before the first header)
+    std::vector<int64_t> span_end;             // cumulative rstripped length after each span
+    std::vector<int64_t> cur((size_t)nj, -1);  // record of the current name per job, -1: not in its PAF
+    bool any = false;
     size_t cur_pos = 0;
+    int valid = -1;  // every byte of the record in ACGTN after upper(): -1 not checked yet
+    char bad_c = '?';
     // copy seq[i0, i1) (upper-cased) to dst, forward
     auto copy_fwd = [&](int64_t i0, int64_t i1, char* dst) {
       size_t j = std::upper_bound(span_end.begin(), span_end.end(), i0) - span_end.begin();
@@ -337,57 +325,68 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
         for (; i < e; ++i) *dst++ = upper(spans[j][(size_t)(i - s0)]);
       }
     };
-    auto done = [&]() {      // :259-265 for the record just read
-      if (cur < 0) return;
-      const PafRec& r = keep[cur];
-      const int64_t L = span_end.empty() ? 0 : span_end.back();
-      if (r.minus) {
-        // "".join([BASE_COMPLIMENT[x.upper()] for x in seq[::-1]]) (:263): a KeyError
-        // for any byte of the WHOLE sequence outside ACGTN (after upper(); for
-        // ASCII, (c & 0xDF) is upper() on letters and maps no other byte onto
-        // A, C, G, T, N).  The first offending byte in seq[::-1] order is reported.
-        bool bad = false;
-        for (const sv& s : spans) {
-          unsigned ok = 1;
-          for (char ch : s) {
-            const unsigned u = (unsigned char)ch & 0xDFu;
-            ok &= (unsigned)((u == 'A') | (u == 'C') | (u == 'G') | (u == 'T') | (u == 'N'));
+    // "".join([BASE_COMPLIMENT[x.upper()] for x in seq[::-1]]) (:263) raises a
+    // KeyError for any byte of the WHOLE sequence outside ACGTN (after upper();
+    // for ASCII, (c & 0xDF) is upper() on letters and maps no other byte onto
+    // A, C, G, T, N); the first offending byte in seq[::-1] order is reported
+    auto check_rc = [&]() {
+      if (valid >= 0) return;
+      bool bad = false;
+      for (const sv& s : spans) {
+        unsigned ok = 1;
+        for (char ch : s) {
+          const unsigned u = (unsigned char)ch & 0xDFu;
+          ok &= (unsigned)((u == 'A') | (u == 'C') | (u == 'G') | (u == 'T') | (u == 'N'));
+        }
+        bad |= !ok;
+      }
+      valid = bad ? 0 : 1;
+      if (bad)
+        for (auto it = spans.rbegin(); it != spans.rend() && bad_c == '?'; ++it)
+          for (size_t i = it->size(); i-- > 0;) {
+            const unsigned u = (unsigned char)(*it)[i] & 0xDFu;
+            if (!(u == 'A' || u == 'C' || u == 'G' || u == 'T' || u == 'N')) { bad_c = upper((*it)[i]); break; }
           }
-          bad |= !ok;
+    };
+    auto done = [&]() {  // :259-265 for the record just read, in every job whose PAF names it
+      if (!any) return;
+      const int64_t L = span_end.empty() ? 0 : span_end.back();
+      for (int j = 0; j < nj; ++j) {
+        const int64_t c = cur[(size_t)j];
+        if (c < 0) continue;
+        Job& J = jobs[(size_t)j];
+        const PafRec& r = J.keep[(size_t)c];
+        if (r.minus) {
+          check_rc();
+          if (!valid) {
+            ffails[(size_t)j][(size_t)k].set(MPC_INGEST_ERROR, cur_pos,
+                                             "KeyError: '" + std::string(1, bad_c) + "' (reverse complement of read " +
+                                                 std::string(r.name.substr(0, 80)) + ")");
+            continue;
+          }
         }
-        if (bad) {
-          char c = '?';
-          for (auto it = spans.rbegin(); it != spans.rend() && c == '?'; ++it)
-            for (size_t i = it->size(); i-- > 0;) {
-              const unsigned u = (unsigned char)(*it)[i] & 0xDFu;
-              if (!(u == 'A' || u == 'C' || u == 'G' || u == 'T' || u == 'N')) { c = upper((*it)[i]); break; }
-            }
-          ffails[k].set(MPC_INGEST_ERROR, cur_pos, "KeyError: '" + std::string(1, c) + "' (reverse complement of read " +
-                                                       std::string(r.name.substr(0, 80)) + ")");
-          return;
+        const int64_t u = py_cut(L, r.qs), d = py_cut(L, r.qe);
+        std::string up((size_t)u, '\0'), down((size_t)(L - d), '\0');
+        if (!r.minus) {
+          copy_fwd(0, u, &up[0]);
+          copy_fwd(d, L, &down[0]);
+        } else {  // rc[i] = comp(seq[L-1-i]): rc[:u] from seq[L-u, L), rc[d:] from seq[0, L-d), both reversed
+          auto comp_rev = [](std::string& s) {
+            std::reverse(s.begin(), s.end());
+            for (char& ch : s) ch = ch == 'A' ? 'T' : ch == 'T' ? 'A' : ch == 'G' ? 'C' : ch == 'C' ? 'G' : 'N';
+          };
+          copy_fwd(L - u, L, &up[0]);
+          comp_rev(up);
+          copy_fwd(0, L - d, &down[0]);
+          comp_rev(down);
         }
-      }
-      const int64_t u = py_cut(L, r.qs), d = py_cut(L, r.qe);
-      std::string up((size_t)u, '\0'), down((size_t)(L - d), '\0');
-      if (!r.minus) {
-        copy_fwd(0, u, &up[0]);
-        copy_fwd(d, L, &down[0]);
-      } else {  // rc[i] = comp(seq[L-1-i]): rc[:u] from seq[L-u, L), rc[d:] from seq[0, L-d), both reversed
-        auto comp_rev = [](std::string& s) {
-          std::reverse(s.begin(), s.end());
-          for (char& c : s) c = c == 'A' ? 'T' : c == 'T' ? 'A' : c == 'G' ? 'C' : c == 'C' ? 'G' : 'N';
-        };
-        copy_fwd(L - u, L, &up[0]);
-        comp_rev(up);
-        copy_fwd(0, L - d, &down[0]);
-        comp_rev(down);
-      }
-      std::lock_guard<std::mutex> g(locks[cur & 63]);
-      Flank& fl = flanks[cur];
-      if (fl.pos == SIZE_MAX || cur_pos > fl.pos) {  // a duplicate name: the last record wins
-        fl.pos = cur_pos;
-        fl.up = std::move(up);
-        fl.down = std::move(down);
+        std::lock_guard<std::mutex> g(locks[(c + 17 * j) & 63]);
+        Flank& fl = J.flanks[(size_t)c];
+        if (fl.pos == SIZE_MAX || cur_pos > fl.pos) {  // a duplicate name: the last record wins
+          fl.pos = cur_pos;
+          fl.up = std::move(up);
+          fl.down = std::move(down);
+        }
       }
     };
     for (size_t x = a; x < b;) {
@@ -397,11 +396,17 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
       if (!line.empty() && line[0] == '>') {
         done();
         const sv name = rstrip(line).substr(1);  // whole header line (:267); "" is never processed (:260)
-        cur = name.empty() ? -1 : lookup(name);
+        any = false;
+        for (int j = 0; j < nj; ++j) {
+          cur[(size_t)j] = (name.empty() || !jobs[(size_t)j].live) ? -1 : jobs[(size_t)j].lookup(name);
+          any |= cur[(size_t)j] >= 0;
+        }
         cur_pos = x;
+        valid = -1;
+        bad_c = '?';
         spans.clear();
         span_end.clear();
-      } else if (cur >= 0) {
+      } else if (any) {
         const sv s = rstrip(line);  // :270
         if (!s.empty()) {
           spans.push_back(s);
@@ -412,33 +417,43 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
     }
     done();
   });
-  for (auto& f : ffails) fail.merge(f);
-  if (fail.code != MPC_INGEST_OK) return finish(fail.code, fail.msg);
+  for (int j = 0; j < nj; ++j)
+    for (auto& f : ffails[(size_t)j]) jobs[(size_t)j].fail.merge(f);
+}
 
-  // ---- pack in PAF first-occurrence order (:292) ----
+// one job's result packed in PAF first-occurrence order (:292)
+void job_pack(Job& J, int T, mpc_ingest_out* out) {
+  const int64_t N = (int64_t)J.keep.size();
   size_t ncs = 0, nup = 0, ndn = 0;
   for (int64_t i = 0; i < N; ++i) {
-    if (flanks[i].pos == SIZE_MAX)  // paf[read_name]["upstream_seq"] -> KeyError (:303)
-      return finish(MPC_INGEST_ERROR, "KeyError: 'upstream_seq' (read " + std::string(keep[i].name.substr(0, 80)) +
+    const PafRec& r = J.keep[(size_t)i];
+    const Flank& f = J.flanks[(size_t)i];
+    if (f.pos == SIZE_MAX) {  // paf[read_name]["upstream_seq"] -> KeyError (:303)
+      J.fail.set(MPC_INGEST_ERROR, 0, "KeyError: 'upstream_seq' (read " + std::string(r.name.substr(0, 80)) +
                                           " not in the reads file)");
-    if (keep[i].ts < 0 || keep[i].ts >= ((int64_t)1 << 31))
-      return finish(MPC_INGEST_ERROR, "target start out of range (unsupported)");
-    ncs += keep[i].cs.size(); nup += flanks[i].up.size(); ndn += flanks[i].down.size();
+      return;
+    }
+    if (r.ts < 0 || r.ts >= ((int64_t)1 << 31)) {
+      J.fail.set(MPC_INGEST_ERROR, 0, "target start out of range (unsupported)");
+      return;
+    }
+    ncs += r.cs.size(); nup += f.up.size(); ndn += f.down.size();
   }
   auto alloc = [](size_t n) { return malloc(n ? n : 1); };
-  out->ref = (uint8_t*)alloc(ref.size());
-  memcpy(out->ref, ref.data(), ref.size());
-  out->ref_len = (int64_t)ref.size();
+  out->ref = (uint8_t*)alloc(J.ref.size());
+  memcpy(out->ref, J.ref.data(), J.ref.size());
+  out->ref_len = (int64_t)J.ref.size();
   out->cs = (uint8_t*)alloc(ncs); out->up = (uint8_t*)alloc(nup); out->down = (uint8_t*)alloc(ndn);
   out->cs_off = (int64_t*)alloc(8 * (N + 1)); out->up_off = (int64_t*)alloc(8 * (N + 1));
   out->down_off = (int64_t*)alloc(8 * (N + 1));
   out->tstart = (int64_t*)alloc(8 * N); out->aligned = (int64_t*)alloc(8 * N);
   size_t oc = 0, ou = 0, od = 0;
   for (int64_t i = 0; i < N; ++i) {  // offsets (serial prefix), then the copies by read ranges on all threads
+    const PafRec& r = J.keep[(size_t)i];
     out->cs_off[i] = (int64_t)oc; out->up_off[i] = (int64_t)ou; out->down_off[i] = (int64_t)od;
-    oc += keep[i].cs.size(); ou += flanks[i].up.size(); od += flanks[i].down.size();
-    out->tstart[i] = keep[i].ts;
-    out->aligned[i] = keep[i].qe - keep[i].qs;
+    oc += r.cs.size(); ou += J.flanks[(size_t)i].up.size(); od += J.flanks[(size_t)i].down.size();
+    out->tstart[i] = r.ts;
+    out->aligned[i] = r.qe - r.qs;
   }
   out->cs_off[N] = (int64_t)oc; out->up_off[N] = (int64_t)ou; out->down_off[N] = (int64_t)od;
   parallel(T, [&](int k) {
@@ -446,14 +461,81 @@ int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_pat
     auto at = [&](size_t x) { return (int64_t)(std::lower_bound(out->cs_off, out->cs_off + N, (int64_t)x) - out->cs_off); };
     const int64_t i0 = at(oc * k / T), i1 = k == T - 1 ? N : at(oc * (k + 1) / T);
     for (int64_t i = i0; i < i1; ++i) {
-      memcpy(out->cs + out->cs_off[i], keep[i].cs.data(), keep[i].cs.size());
-      memcpy(out->up + out->up_off[i], flanks[i].up.data(), flanks[i].up.size());
-      memcpy(out->down + out->down_off[i], flanks[i].down.data(), flanks[i].down.size());
+      memcpy(out->cs + out->cs_off[i], J.keep[(size_t)i].cs.data(), J.keep[(size_t)i].cs.size());
+      memcpy(out->up + out->up_off[i], J.flanks[(size_t)i].up.data(), J.flanks[(size_t)i].up.size());
+      memcpy(out->down + out->down_off[i], J.flanks[(size_t)i].down.data(), J.flanks[(size_t)i].down.size());
     }
   });
   out->n_reads = N;
-  out->n_alignments = n_lines;
-  return finish(MPC_INGEST_OK, "");
+  out->n_alignments = J.n_lines;
+}
+
+}  // namespace
+
+extern "C" {
+
+int mpc_ingest_version(void) { return 3; }  // 3: + mpc_ingest_multi; 2: + mpc_write_calls, mpc_py_float_repr, pseudopair
+
+void mpc_ingest_free(mpc_ingest_out* o) {
+  if (!o) return;
+  free(o->ref); free(o->cs); free(o->cs_off); free(o->tstart); free(o->up); free(o->up_off);
+  free(o->down); free(o->down_off); free(o->aligned);
+  o->ref = o->cs = o->up = o->down = nullptr;
+  o->cs_off = o->tstart = o->up_off = o->down_off = o->aligned = nullptr;
+}
+
+int mpc_ingest_multi(int n_jobs, const char* const* ref_paths, const char* const* paf_paths, const char* reads_path,
+                     int n_threads, mpc_ingest_out* outs) {
+  if (n_jobs <= 0) return MPC_INGEST_OK;
+  for (int j = 0; j < n_jobs; ++j) memset(&outs[j], 0, sizeof(outs[j]));
+  auto finish = [&](mpc_ingest_out* out, int code, const std::string& msg) {
+    out->status = code;
+    snprintf(out->message, sizeof(out->message), "%s", msg.c_str());
+    if (code != MPC_INGEST_OK) mpc_ingest_free(out);
+  };
+  auto finish_all = [&](int code, const std::string& msg) {
+    for (int j = 0; j < n_jobs; ++j) finish(&outs[j], code, msg);
+    return code;
+  };
+  const int T = std::max(1, std::min(n_threads > 0 ? n_threads : host_threads(), 64));
+  std::vector<Job> jobs((size_t)n_jobs);
+  // a job's own errors in the reference's order: its reference, then its PAF,
+  // then the reads file (:161, :192, :253)
+  for (int j = 0; j < n_jobs; ++j) {
+    Job& J = jobs[(size_t)j];
+    if (!J.fr.open(ref_paths[j])) J.fail.set(MPC_INGEST_ERROR, 0, std::string("cannot open ") + ref_paths[j]);
+    else if (!J.fp.open(paf_paths[j])) J.fail.set(MPC_INGEST_ERROR, 0, std::string("cannot open ") + paf_paths[j]);
+    if (J.fail.code != MPC_INGEST_OK) J.live = false;
+  }
+  Mapped fa;
+  const bool fa_ok = fa.open(reads_path);
+  if (fa_ok && needs_python(fa, T))
+    return finish_all(MPC_INGEST_FALLBACK, "non-ASCII byte or carriage return: Python text-mode semantics");
+  for (auto& J : jobs) {
+    if (!J.live) continue;
+    if (needs_python(J.fr, T) || needs_python(J.fp, T)) {
+      J.fail.set(MPC_INGEST_FALLBACK, 0, "non-ASCII byte or carriage return: Python text-mode semantics");
+      J.live = false;
+      continue;
+    }
+    job_ref_paf(J, T);
+    if (J.live && !fa_ok) {
+      J.fail.set(MPC_INGEST_ERROR, 0, std::string("cannot open ") + reads_path);
+      J.live = false;
+    }
+  }
+  if (fa_ok) jobs_fasta(jobs, fa, T);
+  for (int j = 0; j < n_jobs; ++j) {
+    Job& J = jobs[(size_t)j];
+    if (J.fail.code == MPC_INGEST_OK) job_pack(J, T, &outs[j]);
+    finish(&outs[j], J.fail.code, J.fail.msg);
+  }
+  return outs[0].status;
+}
+
+int mpc_ingest(const char* ref_path, const char* paf_path, const char* reads_path, int n_threads,
+               mpc_ingest_out* out) {
+  return mpc_ingest_multi(1, &ref_path, &paf_path, reads_path, n_threads, out);
 }
 
 }  // extern "C"

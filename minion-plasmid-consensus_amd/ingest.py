@@ -141,7 +141,7 @@ class _IngestOut(ctypes.Structure):
 
 
 INGEST_OK, INGEST_ERROR, INGEST_FALLBACK = 0, 1, 2
-INGEST_ABI = 2  # mpc_ingest_version() of the library these bindings expect
+INGEST_ABI = 3  # mpc_ingest_version() of the library these bindings expect
 _ingest_lib = None
 
 
@@ -164,6 +164,9 @@ def _native():
         L.mpc_ingest.restype = ctypes.c_int
         L.mpc_ingest.argtypes = [ctypes.c_char_p, ctypes.c_char_p, ctypes.c_char_p, ctypes.c_int,
                                  ctypes.POINTER(_IngestOut)]
+        L.mpc_ingest_multi.restype = ctypes.c_int
+        L.mpc_ingest_multi.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_char_p),
+                                       ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(_IngestOut)]
         L.mpc_ingest_free.argtypes = [ctypes.POINTER(_IngestOut)]
         L.mpc_write_calls.restype = ctypes.c_int
         L.mpc_write_calls.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p, ctypes.c_char_p,
@@ -178,17 +181,43 @@ def pack_sample_native(ref_path, paf_path, reads_path, n_threads=0):
     """Steps 1-3 through libmpc_ingest.so.  Returns the packed dict, None when the
     native parser declines the input (use :func:`pack_sample_python`), or raises
     :class:`IngestError` where the reference raises."""
+    r = pack_samples_native([(ref_path, paf_path)], reads_path, n_threads)
+    if r is None:
+        return None
+    if isinstance(r[0], IngestError):
+        raise r[0]
+    return r[0]
+
+
+def pack_samples_native(jobs, reads_path, n_threads=0):
+    """Steps 1-3 of several (ref_path, paf_path) jobs against ONE reads FASTA,
+    scanned once (mpc_ingest_multi).  Returns None when the library is missing,
+    else a list with, per job, the packed dict, None (declined: use the Python
+    ingest) or the :class:`IngestError` the reference raises for that job."""
     L = _native()
     if L is None:
         return None
-    own = _IngestBuffers(L)
-    o = own.out
+    nj = len(jobs)
     enc = lambda p: os.fsencode(p)
-    L.mpc_ingest(enc(ref_path), enc(paf_path), enc(reads_path), int(n_threads), ctypes.byref(o))
-    if o.status == INGEST_FALLBACK:
-        return None
-    if o.status != INGEST_OK:
-        raise IngestError(o.message.decode(errors="replace"))
+    refs = (ctypes.c_char_p * nj)(*[enc(r) for r, _ in jobs])
+    pafs = (ctypes.c_char_p * nj)(*[enc(p) for _, p in jobs])
+    outs = (_IngestOut * nj)()
+    L.mpc_ingest_multi(nj, refs, pafs, enc(reads_path), int(n_threads), outs)
+    res = []
+    for j in range(nj):
+        own = _IngestBuffers(L, outs, j)
+        o = own.out
+        if o.status == INGEST_FALLBACK:
+            res.append(None)
+        elif o.status != INGEST_OK:
+            res.append(IngestError(o.message.decode(errors="replace")))
+        else:
+            res.append(_views(own))
+    return res
+
+
+def _views(own):
+    o = own.out
     n = o.n_reads
     # zero-copy: the arrays are views of the library's buffers (a GB of cs at
     # C3), freed once the last view is gone
@@ -207,12 +236,14 @@ def pack_sample_native(ref_path, paf_path, reads_path, n_threads=0):
 
 
 class _IngestBuffers:
-    """Owner of one mpc_ingest result: numpy views of its buffers keep it alive
-    (through their ctypes base), and it frees them when the last view goes."""
+    """Owner of one mpc_ingest result (element j of an output array): numpy views
+    of its buffers keep it alive (through their ctypes base), and it frees them
+    when the last view goes."""
 
-    def __init__(self, lib):
+    def __init__(self, lib, outs, j):
         self.lib = lib
-        self.out = _IngestOut()
+        self.outs = outs  # keeps the array alive
+        self.out = outs[j]
 
     def view(self, ptr, k, ct):
         if k <= 0:
@@ -236,6 +267,29 @@ def pack_sample(ref_path, paf_path, reads_path, native=True):
         if r is not None:
             return r
     return pack_sample_python(ref_path, paf_path, reads_path)
+
+
+def pack_samples(jobs, native=True):
+    """Steps 1-3 for (ref_path, paf_path, reads_path) jobs -> list of packed
+    dicts, in job order.  Jobs sharing a reads file are ingested together (one
+    scan of it); a job the native parser declines takes the Python path.  The
+    first job (in order) the reference would reject raises its IngestError."""
+    out = [None] * len(jobs)
+    if native:
+        groups = {}
+        for j, (_, _, reads) in enumerate(jobs):
+            groups.setdefault(os.fspath(reads), []).append(j)
+        for reads, idx in groups.items():
+            r = pack_samples_native([(jobs[j][0], jobs[j][1]) for j in idx], reads)
+            if r is not None:
+                for j, x in zip(idx, r):
+                    out[j] = x
+    for j, (ref, paf, reads) in enumerate(jobs):
+        if isinstance(out[j], IngestError):
+            raise out[j]
+        if out[j] is None:
+            out[j] = pack_sample_python(ref, paf, reads)
+    return out
 
 
 def pack_sample_python(ref_path, paf_path, reads_path):

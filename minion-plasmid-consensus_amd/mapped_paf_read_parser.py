@@ -86,11 +86,12 @@ def main(argv=None, timings=None):
     jobs += [(r, p, args.READS, c, ch, a) for r, p, c, ch, a in args.also] + [tuple(j) for j in args.job]
     t0 = time.perf_counter()
     try:
-        samples = []
         for ref, paf, reads, *_ in jobs:
             statprint(f"Ingesting {paf} against {ref}...")
-            samples.append(ingest.pack_sample(ref, paf, reads))
-            statprint("There were {} mapped reads.".format(samples[-1]["n_alignments"]))
+        # jobs sharing a reads file are ingested together (one scan of it)
+        samples = ingest.pack_samples([(ref, paf, reads) for ref, paf, reads, *_ in jobs])
+        for s in samples:
+            statprint("There were {} mapped reads.".format(s["n_alignments"]))
         t1 = time.perf_counter()
         tm["ingest"] = t1 - t0
         if args.MIN_DEPTH_FACTOR is None:

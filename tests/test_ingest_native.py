@@ -148,3 +148,27 @@ def test_dups_semantics(ing, tmp_path):
     r = ing.pack_sample(*_files(tmp_path, *EDGE["dups"]))
     assert list(r["aligned"]) == [10, 10]  # 'a' keeps its first PAF line (qs 2, qe 12)
     assert bytes(r["up"][r["up_off"][0]:r["up_off"][1]]) == b"CC"  # the last '>a' record
+
+
+def test_multi_job_shared_reads(ing, tmp_path):
+    """Jobs against one reads file, ingested in one scan, equal the one-job results
+    (including a job the reference rejects and one the native parser declines)."""
+    (tmp_path / "r1.fa").write_text(">r\nACGTACGTAC\n")
+    (tmp_path / "r2.fa").write_text(">r\nGGGGACGTAC\n")
+    reads = tmp_path / "reads.fa"
+    reads.write_text(">a\nTTACGTACGTACGG\n>b\nACGTACGTACGT\n>c\nacgtNCGTAC\n")
+    (tmp_path / "p1.paf").write_text(paf_line("a", 14, 2, 12, "+", 0, ":10") + paf_line("b", 12, 0, 10, "-", 0, ":10"))
+    (tmp_path / "p2.paf").write_text(paf_line("c", 10, 1, 9, "-", 0, ":8") + paf_line("a", 14, 0, 10, "-", 0, ":10"))
+    (tmp_path / "p3.paf").write_text(paf_line("z", 10, 1, 9, "-", 0, ":8"))  # z not in the reads: KeyError
+    jobs = [(str(tmp_path / "r1.fa"), str(tmp_path / "p1.paf"), str(reads)),
+            (str(tmp_path / "r2.fa"), str(tmp_path / "p2.paf"), str(reads))]
+    multi = ing.pack_samples(jobs)
+    for (ref, paf, rd), m in zip(jobs, multi):
+        one = ing.pack_sample_python(ref, paf, rd)
+        for k in ("ref", "cs", "cs_off", "tstart", "up", "up_off", "down", "down_off", "aligned"):
+            assert np.array_equal(np.asarray(m[k]), np.asarray(one[k])), k
+        assert m["n_alignments"] == one["n_alignments"]
+    r = ing.pack_samples_native([(jobs[0][0], jobs[0][1]), (str(tmp_path / "r1.fa"), str(tmp_path / "p3.paf"))], str(reads))
+    assert isinstance(r[0], dict) and isinstance(r[1], ing.IngestError)
+    with pytest.raises(ing.IngestError):
+        ing.pack_samples(jobs + [(str(tmp_path / "r1.fa"), str(tmp_path / "p3.paf"), str(reads))])

@@ -2394,6 +2394,99 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K
   if (blockIdx.x == 0 && threadIdx.x == 0) d.ncalls[d.S] = (int32_t)all;
 }
 
+// keep[row] = emitted (:428) and the ordered compaction of the kept calls in
+// ONE launch: every block publishes its kept count, then chains the counts of
+// the blocks before it by a decoupled look-back (one 64-bit status word per
+// block, {flag, launch epoch, value}: flag 1 = the block's own count, 2 = its
+// inclusive prefix; wave 0 reads 64 predecessors per step and stops at the
+// nearest prefix).  Blocks are dispatched in index order, so a block only ever
+// waits on blocks that are already running or done; the spin is bounded anyway
+// (DE_INTERNAL instead of a hang).  Replaces K_keep + K_emit (two launches and
+// a read of every block count by every block).
+constexpr uint64_t kSelAgg = 1ull << 62, kSelPre = 2ull << 62, kSelTag = 0x3fffffffull << 32;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K_select(Dev d, int64_t R, uint32_t epoch) {
+  __shared__ int32_t srow[kSmpLds];
+  __shared__ uint32_t smd[kSmpLds];
+  __shared__ int32_t s_w[4];
+  __shared__ int64_t s_pre;
+  load_sample_rows(d, srow);
+  for (int s = threadIdx.x; s < d.S && s < kSmpLds; s += blockDim.x) smd[s] = d.maxdepth[s];
+  const int64_t b = blockIdx.x;
+  const int64_t nb = (R + kKB - 1) / kKB;
+  const int64_t base = b * kKB + 4 * threadIdx.x;
+  uint4 v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) v[k] = base + k < R ? reinterpret_cast<const uint4*>(d.res)[base + k] : make_uint4(0, 0, 0, 0);
+  __syncthreads();
+  int c = 0;
+  uint32_t bits = 0;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    if (v[k].x >> 24) {
+      const int s = sample_of_row_lds(d, srow, base + k);
+      const double thr = (double)(s < kSmpLds ? smd[s] : d.maxdepth[s]) * d.mdf;  // :338
+      if ((double)v[k].y > thr) { ++c; bits |= 1u << k; }  // :428
+    }
+  }
+  const int w = threadIdx.x >> 6, l = lane();
+  const int inc = wave_scan_i32(c);
+  if (l == 63) s_w[w] = inc;
+  __syncthreads();
+  int32_t wpre = 0, bt = 0;
+  for (int k = 0; k < 4; ++k) { wpre += k < w ? s_w[k] : 0; bt += s_w[k]; }
+  uint64_t* st = reinterpret_cast<uint64_t*>(d.ksum);
+  const uint64_t tag = (uint64_t)(epoch & 0x3fffffffu) << 32;
+  if (w == 0) {
+    if (l == 0) __hip_atomic_store(st + b, (b == 0 ? kSelPre : kSelAgg) | tag | (uint32_t)bt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int64_t pre = 0;
+    int spins = 0;
+    for (int64_t j0 = b - 1; j0 >= 0;) {
+      const int64_t j = j0 - l;  // lane l: predecessor j0 - l; before block 0: a prefix of 0
+      const uint64_t x = j >= 0 ? __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (kSelPre | tag);
+      const bool ready = (x & kSelTag) == tag && (x >> 62) != 0;
+      const uint64_t rdy = ballot(ready), pfx = ballot(ready && (x >> 62) == 2);
+      const uint64_t need = pfx ? (pfx & (0 - pfx)) * 2 - 1 : ~0ull;  // lanes up to the nearest prefix
+      if ((rdy & need) != need) {
+        if (++spins > (1 << 22)) {  // never expected: in-order dispatch
+          if (l == 0) atomicOr(&d.status[MPC_ST_FLAGS], DE_INTERNAL);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      const int32_t val = ((need >> l) & 1ull) ? (int32_t)(uint32_t)x : 0;
+      pre += wave_sum(val);
+      if (pfx) break;
+      j0 -= 64;
+    }
+    if (l == 0) {
+      if (b > 0) __hip_atomic_store(st + b, kSelPre | tag | (uint32_t)(pre + bt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      s_pre = pre;
+    }
+  }
+  __syncthreads();
+  const int64_t pre = s_pre;
+  int64_t pos = pre + wpre + inc - c;
+#pragma unroll
+  for (int k = 0; k < 4; ++k)
+    if (bits & (1u << k)) {
+      const uint4 x = v[k];
+      reinterpret_cast<uint4*>(d.calls)[pos++] = make_uint4(x.x & 0xffffffu, x.y, x.z, x.w);
+    }
+  // ncalls[s] = calls before the first row of sample s; ncalls[S] = all
+  const int64_t b0 = b * kKB, all = pre + bt;
+  for (int s = 0; s < d.S; ++s) {
+    const int64_t rb = s < kSmpLds ? srow[s] : d.srow[s];
+    if (rb >= b0 && rb < b0 + kKB && (rb - b0) / 4 == threadIdx.x) {
+      int64_t q = pre + wpre + inc - c;
+      for (int k = 0; k < (int)((rb - b0) & 3); ++k) q += (bits >> k) & 1u;
+      d.ncalls[s] = (int32_t)q;
+    }
+    if (b == nb - 1 && threadIdx.x == 0 && rb >= nb * kKB) d.ncalls[s] = (int32_t)all;
+  }
+  if (b == nb - 1 && threadIdx.x == 0) d.ncalls[d.S] = (int32_t)all;
+}
+
 }  // namespace
 
 // ===========================================================================
@@ -2440,6 +2533,7 @@ struct mpc_plan {
   int64_t cnt[B_COUNT];
   bool bound = false;
   bool runt_dirty = true;  // runt may hold tallies: K_clear zeroes it (K_ins zeroes what it maps)
+  uint32_t sel_epoch = 0;  // K_select's look-back tag: one per consensus launch
   Dev dev() const;
 };
 
@@ -2684,6 +2778,10 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     static const int cand[10][2] = {{1, 2048}, {2, 2048}, {1, 1024}, {2, 1024}, {3, 2048}, {3, 1024},
                                     {1, 512}, {0, 2048}, {0, 1024}, {0, 512}};
     int best = -1, per_cu = 1;
+    // tuning override for measurements: MPC_PARSE_GEOMETRY="tm,win,nw" takes that
+    // candidate when it fits the LDS budget (else the planner's choice)
+    int o_tm = -1, o_win = -1, o_nw = -1;
+    if (const char* e = getenv("MPC_PARSE_GEOMETRY")) sscanf(e, "%d,%d,%d", &o_tm, &o_win, &o_nw);
     for (const auto& c : cand)
       for (int nw : {16, 12, 8}) {
         if (c[0] == 3 && !sub_events && best > 0) break;  // global-atomic tm 3 only when nothing else fits
@@ -2691,7 +2789,8 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
         const int lds = lds_of(c[1], c[0], nw);
         if (lds > lds_cap) continue;
         const int wgs = std::max(1, std::min(lds_cap / lds, max_waves_cu / nw));
-        const int score = wgs * nw * (c[1] == 512 ? 75 : c[1] == 1024 ? 95 : 100);
+        int score = wgs * nw * (c[1] == 512 ? 75 : c[1] == 1024 ? 95 : 100);
+        if (c[0] == o_tm && c[1] == o_win && nw == o_nw) score = 1 << 30;
         if (score > best) { best = score; p->tally_mode = c[0]; p->parse_win = c[1]; p->parse_nw = nw; per_cu = wgs; }
       }
     if (best < 0) {
@@ -2877,7 +2976,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_META, (R + 3) / 4 * 4, 1);
   set(mpc_plan::B_RES, R * 4, 4);
   set(mpc_plan::B_KEEP, nbk * 256, 4);
-  set(mpc_plan::B_KSUM, nbk, 4);
+  set(mpc_plan::B_KSUM, nbk, 8);  // K_select's per-block look-back status words
   set(mpc_plan::B_CALLS, R * 4, 4);
   set(mpc_plan::B_NCALLS, p->S + 1, 4);
   set(mpc_plan::B_MAXD, p->S, 4);
@@ -3004,7 +3103,9 @@ int mpc_parse(mpc_plan* p, void* stream) {
   Dev d = p->dev();
   {
     ClearArgs c{};
+    bool over = false;
     auto add = [&](void* ptr, int64_t words, uint32_t v) {
+      if (c.n == 16) { over = true; return; }  // ClearArgs holds 16 ranges
       c.ptr[c.n] = reinterpret_cast<uint32_t*>(ptr); c.words[c.n] = words; c.value[c.n] = v; ++c.n;
     };
     add(d.status, MPC_ST_FIRST_READ, 0u);                // (disjoint ranges: no ordering between threads)
@@ -3017,11 +3118,13 @@ int mpc_parse(mpc_plan* p, void* stream) {
     add(d.maxR, p->G, 0u);
     if (p->tally_mode == 4) add(at<int32_t>(p, mpc_plan::B_BKCUR), (int64_t)p->n_parse_wg * p->nbmax, 0u);
     add(d.maxdepth, p->S, 0u);
+    add(d.ksum, 2 * p->cnt[mpc_plan::B_KSUM], 0u);  // K_select status words (epoch-tagged as well)
     add(d.M, p->runs_cap, 0u);
     add(d.runR, p->runs_cap, 0u);
     if (p->runt_dirty) add(d.runt, 16 * p->runs_cap, 0u);
     add(d.rows, 4 * p->row_cap, 0u);
     add(d.meta, (int64_t)(p->sz[mpc_plan::B_META] / 4), 0u);
+    if (over) return fail(MPC_E_STATE, "K_clear range table overflow");
     const int64_t most = std::max<int64_t>(4 * p->row_cap, std::max<int64_t>(4 * p->G, (p->runt_dirty ? 16 : 1) * p->runs_cap));
     hipLaunchKernelGGL(K_clear, dim3(std::min<unsigned>(nblk(most, 256), 1024)), dim3(256), 0, st, c);
     HIPCHK(hipGetLastError());
@@ -3103,8 +3206,9 @@ int mpc_consensus(mpc_plan* p, double mdf, double gtf, void* stream) {
   const int64_t R = p->row_cap;
   if (nblk(R, 256) > kCallBlocksMax) hipLaunchKernelGGL(K_call<kCRBig>, dim3(nblk(R, 256 * kCRBig)), dim3(256), 0, st, d, R);
   else hipLaunchKernelGGL(K_call<1>, dim3(nblk(R, 256)), dim3(256), 0, st, d, R);
-  hipLaunchKernelGGL(K_keep, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R);
-  hipLaunchKernelGGL(K_emit, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R);
+  p->sel_epoch = (p->sel_epoch + 1) & 0x3fffffffu;
+  if (p->sel_epoch == 0) p->sel_epoch = 1;  // 0 never tags a word (zeroed workspace)
+  hipLaunchKernelGGL(K_select, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R, p->sel_epoch);
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }

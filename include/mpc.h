@@ -12,9 +12,9 @@
  *                                                  mpc_parse()           (K_parse)
  *   processBaseString_leftIndel/rightIndel :37-72  mpc_index() .. mpc_rows()
  *                                                  (even-slot layout, tallies: K_rsplit, K_left,
- *                                                  K_replay, K_ins, K_flank)
- *   Step 5 max depth :332-341                      mpc_consensus()       (K_consensus)
- *   Step 6 consensus/threshold :348-439            mpc_consensus()       (K_consensus, K_emit)
+ *                                                  K_layout, K_ins, K_flank)
+ *   Step 5 max depth :332-341                      mpc_consensus()       (K_call)
+ *   Step 6 consensus/threshold :348-439            mpc_consensus()       (K_call, K_select)
  *   whole Step 4-6                                 mpc_run()
  *
  * Steps 1-3 (FASTA/PAF ingest, :161-277) and Step 7 (writers) stay on the host.
@@ -183,8 +183,8 @@ int mpc_parse(mpc_plan* plan, void* stream);        /* clear; cs -> i_end, LEFT 
 int mpc_index(mpc_plan* plan, void* stream);        /* downstream (RIGHT) events at mixed gaps, stable (gap, read) sort; insertion work units */
 int mpc_runs(mpc_plan* plan, void* stream);         /* shards > 1: global run index space            */
 int mpc_tally(mpc_plan* plan, void* stream);        /* longest LEFT string per run (M)               */
-int mpc_layout(mpc_plan* plan, void* stream);       /* per-gap replay of the slot layout, row counts */
-int mpc_rows(mpc_plan* plan, void* stream);         /* row offsets, depth, odd rows, insertion and flank tallies */
+int mpc_layout(mpc_plan* plan, void* stream);       /* per-gap replay of the slot layout, row counts, row offsets, depth, odd rows */
+int mpc_rows(mpc_plan* plan, void* stream);         /* insertion and flank tallies onto the slot rows */
 int mpc_consensus(mpc_plan* plan, double min_depth_factor, double global_threshold_factor,
                   void* stream);                    /* max depth, calls, compaction            */
 int mpc_run(mpc_plan* plan, double min_depth_factor, double global_threshold_factor, void* stream);

@@ -15,15 +15,17 @@
 //             K_rstart       per-gap ranges in the sorted list, RIGHT run lengths
 //   runs      K_runs, K_runR (several shards) global run index space
 //   tally     K_left         longest LEFT string per run (insertions, upstream flanks)
-//   layout    K_replay       per-gap replay of the slot-layout state of
-//                            processBaseString_* (:37-72) -> row counts
-//   rows      K_assemble     row offsets + depth (block prefixes), odd rows
-//             K_ins, K_flank insertion / flank bases onto their slot rows
+//   layout    K_layout       per-gap replay of the slot-layout state of
+//                            processBaseString_* (:37-72) -> row counts, then
+//                            row offsets + depth (look-back scan), odd rows
+//   rows      K_ins, K_flank insertion / flank bases onto their slot rows
 //   consensus K_call         per-slot top/second/tie/N (:363-439), max depth
-//             K_keep, K_emit threshold test + ordered compaction of the calls
+//             K_select       threshold test + ordered compaction of the calls
+//                            (look-back scan)
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -49,6 +51,10 @@ constexpr int kBW = 64;             // gaps per insertion bucket (K_left workgro
 static_assert(kBW <= 64 && (kBW & (kBW - 1)) == 0, "sorted insertion events hold the gap within its bucket in 6 bits");
 constexpr int kKMax = 8;            // runs per gap tallied in K_left's LDS (others go to HBM)
 constexpr uint32_t kNullGap = 0x3fffffu;
+// decoupled look-back status words (K_layout, K_select): flag in bits 62-63
+// (1 = a block's own sum, 2 = its inclusive prefix), the launch epoch in bits
+// 32-61, the 32-bit value below
+constexpr uint64_t kSelAgg = 1ull << 62, kSelPre = 2ull << 62, kSelTag = 0x3fffffffull << 32;
 
 struct Ovf {  // long insertion (len > kInsInline), tallied by K_flank
   int64_t off;  // absolute byte offset of the inserted bases in cs
@@ -104,11 +110,11 @@ struct Dev {  // device-side views of the plan for the small kernels (passed by 
   int32_t* runR;                     // [Ng+G] per run: length of the RIGHT string closing it
   int32_t* hiR; int32_t* loR;        // [Ng+G] per run: hi seen by its LEFT events, lo seen by its RIGHT event
   int32_t* lo_f; int32_t* rowcnt; int32_t* row_base;
-  int32_t* bsum;                     // [2 * ceil(G / kGB)] block sums of rowcnt, diff
+  int32_t* bsum;                     // [2 * ceil(G / kGB)] x 8 B: K_layout's look-back words (rows, diff)
   uint32_t* rows; uint8_t* meta; int64_t row_cap;
   uint32_t* runt;                    // [Ng+G][4][4] per run: inline insertion bases by slot from the right end
   uint32_t* res; int32_t* keep; int32_t* ksum; uint32_t* calls; int32_t* ncalls; uint32_t* maxdepth;
-  int32_t* srow;                     // [S] first row of every sample (K_assemble)
+  int32_t* srow;                     // [S] first row of every sample (K_layout)
   double mdf, gtf;
 };
 
@@ -1785,15 +1791,28 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
 //   RIGHT len R : base bi -> absolute -lo+bi  ; hi = max(hi, R-lo)
 // Within a run of LEFT events hi is constant, so only the run's longest LEFT
 // string matters (M); run k is closed by the gap's k-th mixed RIGHT event
-// (length runR).  One thread per gap replays its runs; the per-block sums of
-// the row counts and of the depth difference array feed K_assemble's scans.
+// (length runR).  One thread per gap replays its runs; the row counts and the
+// depth difference array are then scanned in the same launch (K_layout).
 // ---------------------------------------------------------------------------
-constexpr int kGB = 256;  // gaps per K_replay / K_assemble block
+constexpr int kGB = 256;  // gaps per K_layout block
 
-__global__ __launch_bounds__(kGB) void K_replay(Dev d) {
+// K_layout = K_replay + K_assemble in ONE launch: the per-gap replay, then the
+// row offsets and depths as block scans chained across blocks by a decoupled
+// look-back (per block two 64-bit status words, rows and depth difference, each
+// {flag, launch epoch, value}: flag 1 = the block's own sum, 2 = its inclusive
+// prefix).  Blocks are dispatched in index order, so a block waits only on
+// running or finished blocks; the spin is bounded (DE_INTERNAL, never a hang).
+// The row capacity is checked per gap (rows that do not fit are not written);
+// the last block sets ROWS_NEEDED and DE_CAP for the re-plan.
+__global__ __launch_bounds__(kGB) void K_layout(Dev d, uint32_t epoch) {
   __shared__ int32_t s_w[2][kGB / 64];
-  const int64_t g = (int64_t)blockIdx.x * kGB + threadIdx.x;
+  __shared__ int64_t s_pre[2];
+  const int64_t b = blockIdx.x;
+  const int64_t nb = (d.G + kGB - 1) / kGB;
+  const int64_t g = b * kGB + threadIdx.x;
   int32_t rc = 0, dv = 0;
+  int s = 0;
+  int64_t p = 0;
   if (g < d.G) {
     const int64_t r0 = (int64_t)d.right_start[g] + g, r1 = (int64_t)d.right_start[g + 1] + g + 1;  // runs of gap g
     int32_t lo = 0, hi = 0;
@@ -1811,110 +1830,103 @@ __global__ __launch_bounds__(kGB) void K_replay(Dev d) {
     const int32_t mr = d.maxR[g];
     if (mr - lo > hi) hi = mr - lo;
     d.lo_f[g] = lo;
-    // rows of a gap = its slots + the odd position after it (if any)
     int lo_s = 0, hi_s = d.S - 1;  // sample of gap g
     while (lo_s < hi_s) {
       const int mid = (lo_s + hi_s + 1) >> 1;
       if (d.gbase[mid] <= g) lo_s = mid; else hi_s = mid - 1;
     }
-    const int64_t p = g - d.gbase[lo_s];
-    rc = lo + hi + (p < d.n_of[lo_s] ? 1 : 0);
+    s = lo_s;
+    p = g - d.gbase[s];
+    rc = lo + hi + (p < d.n_of[s] ? 1 : 0);  // rows of a gap = its slots + the odd position after it
     d.rowcnt[g] = rc;
     dv = d.diff[g];
   }
-  const int w = threadIdx.x >> 6;
-  rc = wave_sum(rc);
-  dv = wave_sum(dv);
-  if (lane() == 0) { s_w[0][w] = rc; s_w[1][w] = dv; }
+  const int w = threadIdx.x >> 6, l = lane();
+  const int ir = wave_scan_i32(rc), id = wave_scan_i32(dv);
+  if (l == 63) { s_w[0][w] = ir; s_w[1][w] = id; }
   __syncthreads();
-  if (threadIdx.x == 0) {
-    int32_t a = 0, b = 0;
-    for (int k = 0; k < kGB / 64; ++k) { a += s_w[0][k]; b += s_w[1][k]; }
-    d.bsum[2 * blockIdx.x] = a;
-    d.bsum[2 * blockIdx.x + 1] = b;
+  int32_t wr = 0, wd = 0, br = 0, bd = 0;
+  for (int k = 0; k < kGB / 64; ++k) {
+    if (k < w) { wr += s_w[0][k]; wd += s_w[1][k]; }
+    br += s_w[0][k];
+    bd += s_w[1][k];
   }
-}
-
-// Block-level exclusive prefix of K_replay's block sums (pair = {rows, diff}).
-// Every block also gets the totals.  Returns {prefix_rows, prefix_diff, total_rows}.
-__device__ __forceinline__ int3 block_prefix_pairs(const int32_t* bsum, int64_t nb, int64_t b, int32_t* s_red) {
-  int64_t pr = 0, pd = 0, tr = 0;
-  for (int64_t k = threadIdx.x; k < nb; k += blockDim.x) {
-    const int32_t x = bsum[2 * k], y = bsum[2 * k + 1];
-    tr += x;
-    if (k < b) { pr += x; pd += y; }
+  uint64_t* st = reinterpret_cast<uint64_t*>(d.bsum);  // [2 nb]: block b's rows word, diff word
+  const uint64_t tag = (uint64_t)(epoch & 0x3fffffffu) << 32;
+  if (w == 0) {
+    if (l == 0) {
+      const uint64_t f = b == 0 ? kSelPre : kSelAgg;
+      __hip_atomic_store(st + 2 * b + 1, f | tag | (uint32_t)bd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(st + 2 * b, f | tag | (uint32_t)br, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    int64_t pr = 0, pd = 0;
+    int spins = 0;
+    for (int64_t j0 = b - 1; j0 >= 0;) {
+      const int64_t j = j0 - l;  // lane l: predecessor j0 - l; before block 0: prefixes of 0
+      uint64_t xr = kSelPre | tag, xd = kSelPre | tag;
+      if (j >= 0) {
+        xr = __hip_atomic_load(st + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        xd = __hip_atomic_load(st + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      // a lane counts once both words carry this launch's tag and the same flag
+      const bool ready = (xr & kSelTag) == tag && (xd & kSelTag) == tag && (xr >> 62) != 0 && (xr >> 62) == (xd >> 62);
+      const uint64_t rdy = ballot(ready), pfx = ballot(ready && (xr >> 62) == 2);
+      const uint64_t need = pfx ? (pfx & (0 - pfx)) * 2 - 1 : ~0ull;  // lanes up to the nearest prefix
+      if ((rdy & need) != need) {
+        if (++spins > (1 << 22)) {  // never expected: in-order dispatch
+          if (l == 0) atomicOr(&d.status[MPC_ST_FLAGS], DE_INTERNAL);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+        continue;
+      }
+      const bool in = (need >> l) & 1ull;
+      pr += wave_sum(in ? (int32_t)(uint32_t)xr : 0);
+      pd += wave_sum(in ? (int32_t)(uint32_t)xd : 0);
+      if (pfx) break;
+      j0 -= 64;
+    }
+    if (l == 0) {
+      if (b > 0) {
+        __hip_atomic_store(st + 2 * b + 1, kSelPre | tag | (uint32_t)(int32_t)(pd + bd), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        __hip_atomic_store(st + 2 * b, kSelPre | tag | (uint32_t)(pr + br), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      s_pre[0] = pr;
+      s_pre[1] = pd;
+    }
   }
-  const int w = threadIdx.x >> 6;
-  const int32_t a0 = wave_sum((int32_t)pr), a1 = wave_sum((int32_t)pd), a2 = wave_sum((int32_t)tr);
   __syncthreads();
-  if (lane() == 0) { s_red[3 * w] = a0; s_red[3 * w + 1] = a1; s_red[3 * w + 2] = a2; }
-  __syncthreads();
-  int3 r = make_int3(0, 0, 0);
-  for (int k = 0; k < (int)(blockDim.x >> 6); ++k) { r.x += s_red[3 * k]; r.y += s_red[3 * k + 1]; r.z += s_red[3 * k + 2]; }
-  return r;
-}
-
-// ---------------------------------------------------------------------------
-// Rows: scans of the row counts (-> row_base) and of the depth difference
-// array (-> depth of odd position p), then the odd-position row of every gap
-// (depth - substitutions matched the reference base, :79) and the slot-0
-// marks.  Slot rows were zeroed by K_clear; the flank / insertion kernels add
-// to them.  Also the ROWS_NEEDED / capacity check (all blocks see the total).
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(kGB) void K_assemble(Dev d) {
-  __shared__ int32_t s_red[3 * (kGB / 64)];
-  __shared__ int32_t s_w[2][kGB / 64];
-  const int64_t nb = (d.G + kGB - 1) / kGB;
-  const int3 pre = block_prefix_pairs(d.bsum, nb, blockIdx.x, s_red);
-  const int64_t tot = pre.z;
-  if (blockIdx.x == 0 && threadIdx.x == 0) {
+  const int64_t pre_r = s_pre[0], pre_d = s_pre[1];
+  if (b == nb - 1 && threadIdx.x == 0) {
+    const int64_t tot = pre_r + br;
     d.status[MPC_ST_ROWS_NEEDED] = (uint32_t)tot;
     if (tot > d.row_cap) atomicOr(&d.status[MPC_ST_FLAGS], DE_CAP);
   }
-  const int64_t g = (int64_t)blockIdx.x * kGB + threadIdx.x;
-  const int32_t rc = g < d.G ? d.rowcnt[g] : 0;
-  const int32_t dv = g < d.G ? d.diff[g] : 0;
-  const int w = threadIdx.x >> 6;
-  const int ir = wave_scan_i32(rc), id = wave_scan_i32(dv);
-  if (lane() == 63) { s_w[0][w] = ir; s_w[1][w] = id; }
-  __syncthreads();
-  int32_t wr = 0, wd = 0;
-  for (int k = 0; k < w; ++k) { wr += s_w[0][k]; wd += s_w[1][k]; }
   if (g >= d.G) return;
-  const int64_t rb = (int64_t)pre.x + wr + ir - rc;  // exclusive
-  const int64_t dep = (int64_t)pre.y + wd + id;      // inclusive
+  const int64_t rb = pre_r + wr + ir - rc;  // exclusive
+  const int64_t dep = pre_d + wd + id;      // inclusive
   d.row_base[g] = (int32_t)rb;
-  int lo_s = 0, hi_s = d.S - 1;
-  while (lo_s < hi_s) {
-    const int mid = (lo_s + hi_s + 1) >> 1;
-    if (d.gbase[mid] <= g) lo_s = mid; else hi_s = mid - 1;
-  }
-  const int s = lo_s;
-  const int64_t p = g - d.gbase[s];
   if (p == 0) d.srow[s] = (int32_t)rb;  // the consensus kernels' sample table (one load, no gbase chain)
-  if (tot > d.row_cap) return;
+  if (rb + rc > d.row_cap) return;      // does not fit: the last block flags DE_CAP (re-plan)
   const int64_t n = d.n_of[s];
   const int64_t nslots = (int64_t)rc - (p < n ? 1 : 0);
   if (nslots > 0) d.meta[rb] = 2;  // first slot of the gap
   if (p < n) {
-    uint4 out = make_uint4(0, 0, 0, 0);
-    {  // each shard: its own reads' depth and substitutions (rows are summed over shards)
-      // odd position p: depth = reads covering p with a match or substitution
-      const uint32_t* sb = d.sub + g * 4;
-      const uint32_t s0 = sb[0], s1 = sb[1], s2 = sb[2], s3 = sb[3];
-      const int64_t match = dep - (int64_t)s0 - s1 - s2 - s3;
-      uint32_t c[4] = {s0, s1, s2, s3};
-      uint32_t fl = 0;
-      if (match < 0) fl |= DE_INTERNAL;
-      else if (match > 0) {
-        const int rcode = base_code_exact(d.ref[d.ref_off[s] + p]);
-        if (rcode < 0) fl |= DE_KEY;  // refarr base not in the dict (:61)
-        else c[rcode] += (uint32_t)match;
-      }
-      if (fl) atomicOr(&d.status[MPC_ST_FLAGS], fl);
-      out = make_uint4(c[0], c[1], c[2], c[3]);
+    // each shard: its own reads' depth and substitutions (rows are summed over shards)
+    // odd position p: depth = reads covering p with a match or substitution
+    const uint32_t* sb = d.sub + g * 4;
+    const uint32_t s0 = sb[0], s1 = sb[1], s2 = sb[2], s3 = sb[3];
+    const int64_t match = dep - (int64_t)s0 - s1 - s2 - s3;
+    uint32_t c[4] = {s0, s1, s2, s3};
+    uint32_t fl = 0;
+    if (match < 0) fl |= DE_INTERNAL;
+    else if (match > 0) {
+      const int rcode = base_code_exact(d.ref[d.ref_off[s] + p]);
+      if (rcode < 0) fl |= DE_KEY;  // refarr base not in the dict (:61)
+      else c[rcode] += (uint32_t)match;
     }
-    reinterpret_cast<uint4*>(d.rows)[rb + nslots] = out;
+    if (fl) atomicOr(&d.status[MPC_ST_FLAGS], fl);
+    reinterpret_cast<uint4*>(d.rows)[rb + nslots] = make_uint4(c[0], c[1], c[2], c[3]);
     d.meta[rb + nslots] = 3;  // odd row, first (only) slot of its position
   }
 }
@@ -2314,85 +2326,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K
   }
 }
 
-// keep[row] = emitted (:428) and per-block counts (kKB rows per block)
-constexpr int kKB = 1024;  // rows per K_keep / K_emit block (4 per thread)
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K_keep(Dev d, int64_t R) {
-  __shared__ int32_t srow[kSmpLds];
-  __shared__ uint32_t smd[kSmpLds];
-  __shared__ int32_t s_w[4];
-  load_sample_rows(d, srow);
-  for (int s = threadIdx.x; s < d.S && s < kSmpLds; s += blockDim.x) smd[s] = d.maxdepth[s];
-  const int64_t base = (int64_t)blockIdx.x * kKB + 4 * threadIdx.x;
-  uint4 v[4];
-#pragma unroll
-  for (int k = 0; k < 4; ++k) v[k] = base + k < R ? reinterpret_cast<const uint4*>(d.res)[base + k] : make_uint4(0, 0, 0, 0);
-  __syncthreads();
-  int c = 0;
-  uint32_t bits = 0;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (v[k].x >> 24) {
-      const int s = sample_of_row_lds(d, srow, base + k);
-      const double thr = (double)(s < kSmpLds ? smd[s] : d.maxdepth[s]) * d.mdf;  // :338
-      if ((double)v[k].y > thr) { ++c; bits |= 1u << k; }  // :428
-    }
-  }
-  d.keep[(int64_t)blockIdx.x * 256 + threadIdx.x] = (int32_t)bits;
-  c = wave_sum(c);
-  if (lane() == 0) s_w[threadIdx.x >> 6] = c;
-  __syncthreads();
-  if (threadIdx.x == 0) d.ksum[blockIdx.x] = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-}
-
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K_emit(Dev d, int64_t R) {
-  __shared__ int32_t s_red[4], s_w[4];
-  __shared__ int32_t srow[kSmpLds];
-  load_sample_rows(d, srow);  // (ordered before use by the barriers below)
-  const int64_t nb = (R + kKB - 1) / kKB;
-  int64_t pre = 0, all = 0;
-  for (int64_t k = threadIdx.x; k < nb; k += blockDim.x) {
-    const int32_t x = d.ksum[k];
-    all += x;
-    if (k < (int64_t)blockIdx.x) pre += x;
-  }
-  const int w = threadIdx.x >> 6;
-  {
-    const int32_t a0 = wave_sum((int32_t)pre), a1 = wave_sum((int32_t)all);
-    if (lane() == 0) { s_red[w] = a0; s_w[w] = a1; }
-    __syncthreads();
-    pre = s_red[0] + s_red[1] + s_red[2] + s_red[3];
-    all = s_w[0] + s_w[1] + s_w[2] + s_w[3];
-    __syncthreads();
-  }
-  const uint32_t bits = (uint32_t)d.keep[(int64_t)blockIdx.x * 256 + threadIdx.x];
-  const int c = __popc(bits);
-  const int inc = wave_scan_i32(c);
-  if (lane() == 63) s_red[w] = inc;
-  __syncthreads();
-  int wpre = 0;
-  for (int k = 0; k < w; ++k) wpre += s_red[k];
-  int64_t pos = pre + wpre + inc - c;
-  const int64_t base = (int64_t)blockIdx.x * kKB + 4 * threadIdx.x;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) {
-    if (bits & (1u << k)) {
-      const uint4 v = reinterpret_cast<const uint4*>(d.res)[base + k];
-      reinterpret_cast<uint4*>(d.calls)[pos++] = make_uint4(v.x & 0xffffffu, v.y, v.z, v.w);
-    }
-  }
-  // ncalls[s] = calls before the first row of sample s; ncalls[S] = all
-  const int64_t b0 = (int64_t)blockIdx.x * kKB;
-  for (int s = 0; s < d.S; ++s) {
-    const int64_t rb = s < kSmpLds ? srow[s] : d.srow[s];
-    if (rb >= b0 && rb < b0 + kKB && (rb - b0) / 4 == threadIdx.x) {
-      int64_t q = pre + wpre + inc - c;
-      for (int k = 0; k < (int)((rb - b0) & 3); ++k) q += (bits >> k) & 1u;
-      d.ncalls[s] = (int32_t)q;
-    }
-    if (blockIdx.x == 0 && threadIdx.x == 0 && rb >= nb * kKB) d.ncalls[s] = (int32_t)all;
-  }
-  if (blockIdx.x == 0 && threadIdx.x == 0) d.ncalls[d.S] = (int32_t)all;
-}
+constexpr int kKB = 1024;  // rows per K_select block (4 per thread)
 
 // keep[row] = emitted (:428) and the ordered compaction of the kept calls in
 // ONE launch: every block publishes its kept count, then chains the counts of
@@ -2403,7 +2337,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K
 // waits on blocks that are already running or done; the spin is bounded anyway
 // (DE_INTERNAL instead of a hang).  Replaces K_keep + K_emit (two launches and
 // a read of every block count by every block).
-constexpr uint64_t kSelAgg = 1ull << 62, kSelPre = 2ull << 62, kSelTag = 0x3fffffffull << 32;
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K_select(Dev d, int64_t R, uint32_t epoch) {
   __shared__ int32_t srow[kSmpLds];
   __shared__ uint32_t smd[kSmpLds];
@@ -2493,6 +2426,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K
 // Host side: plan, workspace layout, phases, C-ABI
 // ===========================================================================
 static thread_local std::string g_err;
+// look-back launch epochs (K_layout, K_select): one process-wide sequence, so a
+// status word another plan left in reused memory never carries a live tag; 0 is
+// never used (zeroed words)
+static uint32_t next_epoch() {
+  static std::atomic<uint32_t> e{0};
+  uint32_t v;
+  do v = (e.fetch_add(1) + 1) & 0x3fffffffu; while (v == 0);
+  return v;
+}
 static int fail(int code, const std::string& msg) { g_err = msg; return code; }
 
 #define HIPCHK(x)                                                                  \
@@ -2533,7 +2475,6 @@ struct mpc_plan {
   int64_t cnt[B_COUNT];
   bool bound = false;
   bool runt_dirty = true;  // runt may hold tallies: K_clear zeroes it (K_ins zeroes what it maps)
-  uint32_t sel_epoch = 0;  // K_select's look-back tag: one per consensus launch
   Dev dev() const;
 };
 
@@ -2685,9 +2626,9 @@ static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
 
 // One launch clears every accumulator of a run (status, bitmaps, tallies, rows).
 struct ClearArgs {
-  uint32_t* ptr[16];
-  int64_t words[16];
-  uint32_t value[16];
+  uint32_t* ptr[24];
+  int64_t words[24];
+  uint32_t value[24];
   int32_t n;
 };
 __global__ __launch_bounds__(256) void K_clear(ClearArgs c) {
@@ -2971,7 +2912,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_LOF, G, 4);
   set(mpc_plan::B_ROWCNT, G, 4);
   set(mpc_plan::B_ROWBASE, G, 4);
-  set(mpc_plan::B_BSUM, 2 * nbg, 4);
+  set(mpc_plan::B_BSUM, 2 * nbg, 8);  // K_layout's look-back status words (rows, diff) per block
   set(mpc_plan::B_ROWS, R * 4, 4);
   set(mpc_plan::B_META, (R + 3) / 4 * 4, 1);
   set(mpc_plan::B_RES, R * 4, 4);
@@ -3105,7 +3046,7 @@ int mpc_parse(mpc_plan* p, void* stream) {
     ClearArgs c{};
     bool over = false;
     auto add = [&](void* ptr, int64_t words, uint32_t v) {
-      if (c.n == 16) { over = true; return; }  // ClearArgs holds 16 ranges
+      if (c.n == 24) { over = true; return; }  // ClearArgs holds 24 ranges
       c.ptr[c.n] = reinterpret_cast<uint32_t*>(ptr); c.words[c.n] = words; c.value[c.n] = v; ++c.n;
     };
     add(d.status, MPC_ST_FIRST_READ, 0u);                // (disjoint ranges: no ordering between threads)
@@ -3118,7 +3059,8 @@ int mpc_parse(mpc_plan* p, void* stream) {
     add(d.maxR, p->G, 0u);
     if (p->tally_mode == 4) add(at<int32_t>(p, mpc_plan::B_BKCUR), (int64_t)p->n_parse_wg * p->nbmax, 0u);
     add(d.maxdepth, p->S, 0u);
-    add(d.ksum, 2 * p->cnt[mpc_plan::B_KSUM], 0u);  // K_select status words (epoch-tagged as well)
+    add(d.ksum, 2 * p->cnt[mpc_plan::B_KSUM], 0u);  // look-back status words (epoch-tagged as well)
+    add(d.bsum, 2 * p->cnt[mpc_plan::B_BSUM], 0u);
     add(d.M, p->runs_cap, 0u);
     add(d.runR, p->runs_cap, 0u);
     if (p->runt_dirty) add(d.runt, 16 * p->runs_cap, 0u);
@@ -3179,7 +3121,7 @@ int mpc_layout(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  hipLaunchKernelGGL(K_replay, dim3(nblk(p->G, kGB)), dim3(kGB), 0, st, d);
+  hipLaunchKernelGGL(K_layout, dim3(nblk(p->G, kGB)), dim3(kGB), 0, st, d, next_epoch());
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -3188,7 +3130,6 @@ int mpc_rows(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  hipLaunchKernelGGL(K_assemble, dim3(nblk(p->G, kGB)), dim3(kGB), 0, st, d);
   hipLaunchKernelGGL(K_ins, dim3(ins_grid(p)), dim3(kUB), 0, st, ins_args(p, d));
   HIPCHK(hipGetLastError());
   p->runt_dirty = false;  // K_ins (enqueued) zeroes every run tally it maps (all runs of all gaps)
@@ -3206,9 +3147,7 @@ int mpc_consensus(mpc_plan* p, double mdf, double gtf, void* stream) {
   const int64_t R = p->row_cap;
   if (nblk(R, 256) > kCallBlocksMax) hipLaunchKernelGGL(K_call<kCRBig>, dim3(nblk(R, 256 * kCRBig)), dim3(256), 0, st, d, R);
   else hipLaunchKernelGGL(K_call<1>, dim3(nblk(R, 256)), dim3(256), 0, st, d, R);
-  p->sel_epoch = (p->sel_epoch + 1) & 0x3fffffffu;
-  if (p->sel_epoch == 0) p->sel_epoch = 1;  // 0 never tags a word (zeroed workspace)
-  hipLaunchKernelGGL(K_select, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R, p->sel_epoch);
+  hipLaunchKernelGGL(K_select, dim3(nblk(R, kKB)), dim3(256), 0, st, d, R, next_epoch());
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }

@@ -56,6 +56,73 @@ constexpr uint32_t kNullGap = 0x3fffffu;
 // 32-61, the 32-bit value below
 constexpr uint64_t kSelAgg = 1ull << 62, kSelPre = 2ull << 62, kSelTag = 0x3fffffffull << 32;
 
+// Decoupled look-back, called by ONE wave of block b: publishes the block's NV
+// values (own[k], flag 1), sums its predecessors' values back to the nearest
+// inclusive prefix, publishes its own inclusive prefix (flag 2) and returns the
+// exclusive prefixes in pre[k].  Block b's NV words are st[NV*b .. NV*b+NV-1]; a
+// predecessor counts once all its words carry this launch's tag and the same
+// flag.  Each step reads 64 x U predecessors (U per lane), so a prefix far back
+// is reached in few dependent round trips (2.8 k blocks at C5: 11 steps of 256
+// instead of 44 of 64).  Blocks are dispatched in index order, so the blocks
+// waited on are running or done; the spin is bounded anyway (DE_INTERNAL).
+template <int NV, int U>
+__device__ void lookback(uint64_t* st, int64_t b, uint64_t tag, const int32_t* own, int64_t* pre, uint32_t* flags) {
+  const int l = lane();
+  if (l == 0)
+    for (int k = NV - 1; k >= 0; --k)
+      __hip_atomic_store(st + NV * b + k, (b == 0 ? kSelPre : kSelAgg) | tag | (uint32_t)own[k], __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  int64_t acc[NV];
+  for (int k = 0; k < NV; ++k) acc[k] = 0;
+  int spins = 0;
+  for (int64_t j0 = b - 1; j0 >= 0;) {
+    uint64_t x[U][NV];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t j = j0 - 64 * u - l;  // distance 64 u + l; before block 0: prefixes of 0
+#pragma unroll
+      for (int k = 0; k < NV; ++k)
+        x[u][k] = j >= 0 ? __hip_atomic_load(st + NV * j + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (kSelPre | tag);
+    }
+    // windows u = 0.. in order of distance: every predecessor up to the nearest
+    // prefix must be ready
+    bool ok = true, found = false;
+    uint64_t need[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      bool ready = (x[u][0] & kSelTag) == tag && (x[u][0] >> 62) != 0;
+#pragma unroll
+      for (int k = 1; k < NV; ++k) ready = ready && (x[u][k] & kSelTag) == tag && (x[u][k] >> 62) == (x[u][0] >> 62);
+      const uint64_t rdy = ballot(ready), pfx = ballot(ready && (x[u][0] >> 62) == 2);
+      need[u] = found ? 0ull : (pfx ? (pfx & (0 - pfx)) * 2 - 1 : ~0ull);
+      ok = ok && (rdy & need[u]) == need[u];
+      found = found || pfx != 0;
+    }
+    if (!ok) {
+      if (++spins > (1 << 22)) {  // never expected: in-order dispatch
+        if (l == 0) atomicOr(flags, (uint32_t)MPC_DE_INTERNAL);
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+      continue;
+    }
+#pragma unroll
+    for (int k = 0; k < NV; ++k) {
+      int32_t v = 0;
+#pragma unroll
+      for (int u = 0; u < U; ++u) v += ((need[u] >> l) & 1ull) ? (int32_t)(uint32_t)x[u][k] : 0;
+      acc[k] += wave_sum(v);
+    }
+    if (found) break;
+    j0 -= 64 * U;
+  }
+  if (l == 0 && b > 0)
+    for (int k = NV - 1; k >= 0; --k)
+      __hip_atomic_store(st + NV * b + k, kSelPre | tag | (uint32_t)(int32_t)(acc[k] + own[k]), __ATOMIC_RELAXED,
+                         __HIP_MEMORY_SCOPE_AGENT);
+  for (int k = 0; k < NV; ++k) pre[k] = acc[k];
+}
+
 struct Ovf {  // long insertion (len > kInsInline), tallied by K_flank
   int64_t off;  // absolute byte offset of the inserted bases in cs
   int32_t read;
@@ -1851,49 +1918,12 @@ __global__ __launch_bounds__(kGB) void K_layout(Dev d, uint32_t epoch) {
     br += s_w[0][k];
     bd += s_w[1][k];
   }
-  uint64_t* st = reinterpret_cast<uint64_t*>(d.bsum);  // [2 nb]: block b's rows word, diff word
   const uint64_t tag = (uint64_t)(epoch & 0x3fffffffu) << 32;
-  if (w == 0) {
-    if (l == 0) {
-      const uint64_t f = b == 0 ? kSelPre : kSelAgg;
-      __hip_atomic_store(st + 2 * b + 1, f | tag | (uint32_t)bd, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(st + 2 * b, f | tag | (uint32_t)br, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    int64_t pr = 0, pd = 0;
-    int spins = 0;
-    for (int64_t j0 = b - 1; j0 >= 0;) {
-      const int64_t j = j0 - l;  // lane l: predecessor j0 - l; before block 0: prefixes of 0
-      uint64_t xr = kSelPre | tag, xd = kSelPre | tag;
-      if (j >= 0) {
-        xr = __hip_atomic_load(st + 2 * j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        xd = __hip_atomic_load(st + 2 * j + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      // a lane counts once both words carry this launch's tag and the same flag
-      const bool ready = (xr & kSelTag) == tag && (xd & kSelTag) == tag && (xr >> 62) != 0 && (xr >> 62) == (xd >> 62);
-      const uint64_t rdy = ballot(ready), pfx = ballot(ready && (xr >> 62) == 2);
-      const uint64_t need = pfx ? (pfx & (0 - pfx)) * 2 - 1 : ~0ull;  // lanes up to the nearest prefix
-      if ((rdy & need) != need) {
-        if (++spins > (1 << 22)) {  // never expected: in-order dispatch
-          if (l == 0) atomicOr(&d.status[MPC_ST_FLAGS], DE_INTERNAL);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      const bool in = (need >> l) & 1ull;
-      pr += wave_sum(in ? (int32_t)(uint32_t)xr : 0);
-      pd += wave_sum(in ? (int32_t)(uint32_t)xd : 0);
-      if (pfx) break;
-      j0 -= 64;
-    }
-    if (l == 0) {
-      if (b > 0) {
-        __hip_atomic_store(st + 2 * b + 1, kSelPre | tag | (uint32_t)(int32_t)(pd + bd), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        __hip_atomic_store(st + 2 * b, kSelPre | tag | (uint32_t)(pr + br), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      s_pre[0] = pr;
-      s_pre[1] = pd;
-    }
+  if (w == 0) {  // [2 nb] words: block b's rows word, diff word
+    const int32_t own[2] = {br, bd};
+    int64_t pre[2];
+    lookback<2, 4>(reinterpret_cast<uint64_t*>(d.bsum), b, tag, own, pre, &d.status[MPC_ST_FLAGS]);
+    if (l == 0) { s_pre[0] = pre[0]; s_pre[1] = pre[1]; }
   }
   __syncthreads();
   const int64_t pre_r = s_pre[0], pre_d = s_pre[1];
@@ -2367,35 +2397,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K
   __syncthreads();
   int32_t wpre = 0, bt = 0;
   for (int k = 0; k < 4; ++k) { wpre += k < w ? s_w[k] : 0; bt += s_w[k]; }
-  uint64_t* st = reinterpret_cast<uint64_t*>(d.ksum);
   const uint64_t tag = (uint64_t)(epoch & 0x3fffffffu) << 32;
   if (w == 0) {
-    if (l == 0) __hip_atomic_store(st + b, (b == 0 ? kSelPre : kSelAgg) | tag | (uint32_t)bt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    int64_t pre = 0;
-    int spins = 0;
-    for (int64_t j0 = b - 1; j0 >= 0;) {
-      const int64_t j = j0 - l;  // lane l: predecessor j0 - l; before block 0: a prefix of 0
-      const uint64_t x = j >= 0 ? __hip_atomic_load(st + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : (kSelPre | tag);
-      const bool ready = (x & kSelTag) == tag && (x >> 62) != 0;
-      const uint64_t rdy = ballot(ready), pfx = ballot(ready && (x >> 62) == 2);
-      const uint64_t need = pfx ? (pfx & (0 - pfx)) * 2 - 1 : ~0ull;  // lanes up to the nearest prefix
-      if ((rdy & need) != need) {
-        if (++spins > (1 << 22)) {  // never expected: in-order dispatch
-          if (l == 0) atomicOr(&d.status[MPC_ST_FLAGS], DE_INTERNAL);
-          break;
-        }
-        __builtin_amdgcn_s_sleep(1);
-        continue;
-      }
-      const int32_t val = ((need >> l) & 1ull) ? (int32_t)(uint32_t)x : 0;
-      pre += wave_sum(val);
-      if (pfx) break;
-      j0 -= 64;
-    }
-    if (l == 0) {
-      if (b > 0) __hip_atomic_store(st + b, kSelPre | tag | (uint32_t)(pre + bt), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      s_pre = pre;
-    }
+    int64_t pr;
+    lookback<1, 4>(reinterpret_cast<uint64_t*>(d.ksum), b, tag, &bt, &pr, &d.status[MPC_ST_FLAGS]);
+    if (l == 0) s_pre = pr;
   }
   __syncthreads();
   const int64_t pre = s_pre;

@@ -175,8 +175,9 @@ def e2e_cli(pkg, cfg, reps=2):
 
 
 # what bounds K_parse by its counters (profiles/r03_stalls_*)
-LIMITER = ("latency/issue: far below the HBM roof; SQ counters in profiles/r03_stalls_c2, r03_stalls_c3 "
-           "(DESIGN.md §3)")
+LIMITER = ("dependency latency of the per-round chain (three dependent LDS round trips and a DPP scan per 64 "
+           "units): waves parked on s_waitcnt 47 %, VALU at 30-50 % of its measured 4-wave rate "
+           "(profiles/r03_stalls_*, profiles/r03_micro; DESIGN.md §3)")
 
 
 def batch_l3_resident(cfg):

@@ -1861,7 +1861,13 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
 // (length runR).  One thread per gap replays its runs; the row counts and the
 // depth difference array are then scanned in the same launch (K_layout).
 // ---------------------------------------------------------------------------
-constexpr int kGB = 256;  // gaps per K_layout block
+#ifndef MPC_LAYOUT_GAPS
+#define MPC_LAYOUT_GAPS 256
+#endif
+#ifndef MPC_LOOKBACK_U
+#define MPC_LOOKBACK_U 1
+#endif
+constexpr int kGB = MPC_LAYOUT_GAPS;  // gaps per K_layout block (fewer blocks: a shorter look-back chain)
 
 // K_layout = K_replay + K_assemble in ONE launch: the per-gap replay, then the
 // row offsets and depths as block scans chained across blocks by a decoupled
@@ -1922,7 +1928,7 @@ __global__ __launch_bounds__(kGB) void K_layout(Dev d, uint32_t epoch) {
   if (w == 0) {  // [2 nb] words: block b's rows word, diff word
     const int32_t own[2] = {br, bd};
     int64_t pre[2];
-    lookback<2, 4>(reinterpret_cast<uint64_t*>(d.bsum), b, tag, own, pre, &d.status[MPC_ST_FLAGS]);
+    lookback<2, MPC_LOOKBACK_U>(reinterpret_cast<uint64_t*>(d.bsum), b, tag, own, pre, &d.status[MPC_ST_FLAGS]);
     if (l == 0) { s_pre[0] = pre[0]; s_pre[1] = pre[1]; }
   }
   __syncthreads();
@@ -2400,7 +2406,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K
   const uint64_t tag = (uint64_t)(epoch & 0x3fffffffu) << 32;
   if (w == 0) {
     int64_t pr;
-    lookback<1, 4>(reinterpret_cast<uint64_t*>(d.ksum), b, tag, &bt, &pr, &d.status[MPC_ST_FLAGS]);
+    lookback<1, MPC_LOOKBACK_U>(reinterpret_cast<uint64_t*>(d.ksum), b, tag, &bt, &pr, &d.status[MPC_ST_FLAGS]);
     if (l == 0) s_pre = pr;
   }
   __syncthreads();

@@ -9,7 +9,7 @@ for c in "$@"; do
   mkdir -p $OUT
   for P in FETCH_SIZE WRITE_SIZE; do
     timeout -s KILL 200 rocprofv3 --kernel-trace --pmc $P -d $OUT/$P -o run --output-format csv -- \
-      python3 $R/bench.py --config $c --steps 2 --warmup 1 --kernel-reps 3 --no-cpu-baseline --no-e2e > $OUT/$P.log 2>&1 || { echo "$c $P failed"; tail -5 $OUT/$P.log; exit 1; }
+      python3 $R/bench.py --config $c --steps 2 --warmup 1 --kernel-reps 3 --no-cpu-baseline --no-e2e --hbm-config "" > $OUT/$P.log 2>&1 || { echo "$c $P failed"; tail -5 $OUT/$P.log; exit 1; }
   done
   python3 $R/scripts/traffic.py $OUT K_parse $c $R/gpurun_out/pmc_traffic_$c.json || exit 1
 done

@@ -17,6 +17,13 @@ exactly those reads of the full set) and the ranks exchange the small per-gap
   c3           strong scaling: 1M reads in total, N slices (BASELINE configs[2])
   c5           sample-partitioned replicas: 12 plasmids per GPU, no collective
 
+Batches in flight (--inflight R, default 2): R independent pipelines (each its
+own device copy of the batch and its own workspace) on R streams, taken in
+turn, so one batch's latency-bound post-parse chain overlaps the next batch's
+parse -- a stream of plasmid batches as a sequencing run produces them.  Every
+step is still one full pass of the hot path over one batch; value = aligned
+bases of all K steps / wall time.  --inflight 1 runs them one after another.
+
 Output: one JSON line (rank 0) with the contract fields plus
   roofline      the dominant kernel (K_parse) vs the HBM roofline: algorithmic
                 bytes (sum of cs bytes + 24 B per read) / its mean
@@ -231,6 +238,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--kernel-reps", type=int, default=20)
+    ap.add_argument("--inflight", type=int, default=2,
+                    help="batches in flight (independent pipelines on their own streams, taken in turn)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--hbm-config", default="c3",
@@ -260,11 +269,27 @@ def main():
     cfg = args.config
     n, reads, scaling, profile, seed, antisense, desc = CONFIGS[cfg]
     samples, global_reads = shard_samples(pkg, cfg, rank, world)
-    if world > 1 and cfg != "c5":
-        dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
-        runner = dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange())
-    else:
-        runner = eng.Runner(samples, device=local)
+    # batches in flight: R independent pipelines (own device copy of the batch,
+    # own workspace) on R streams, taken in turn, so one batch's latency-bound
+    # post-parse chain overlaps the next batch's parse (a stream of plasmid
+    # batches, as a sequencing run produces; every step is still one full pass
+    # over one batch)
+    R = max(1, args.inflight)
+
+    def make_runner():
+        if world > 1 and cfg != "c5":
+            dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
+            return dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange())
+        return eng.Runner(samples, device=local)
+
+    runners = [make_runner() for _ in range(R)]
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(R - 1)]
+    runner = runners[0]
+
+    def step(k):
+        with torch.cuda.stream(streams[k % R]):
+            runners[k % R].step(mdf, gtf)
+
     batch = runner.batch
     aligned = batch.aligned_bases
     coll_dev = "cuda" if backend == "nccl" else "cpu"
@@ -274,10 +299,11 @@ def main():
         aligned = int(t.item())
 
     mdf, gtf = 0.1, 5.0  # config.yaml:38-39 (MIN_BASE_FACTOR, GLOBAL_THRESHOLD_FACTOR)
-    for _ in range(max(1, args.warmup)):
-        runner.step(mdf, gtf)
-    runner.check()  # data-error flags must be clear (valid synthetic input)
+    for k in range(max(1, args.warmup) * R):
+        step(k)
     torch.cuda.synchronize()
+    for r in runners:
+        r.check()  # data-error flags must be clear (valid synthetic input)
 
     def barrier():
         if world > 1:
@@ -286,8 +312,8 @@ def main():
     barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        runner.step(mdf, gtf)
+    for k in range(args.steps):
+        step(k)
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
@@ -310,7 +336,8 @@ def main():
     k_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
     runner.step(mdf, gtf)  # leave the plan in a clean state
     torch.cuda.synchronize()
-    runner.check()
+    for r in runners:
+        r.check()
     geo = plan.info()
     alg_bytes = batch.cs_bytes + 24 * batch.n_reads
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
@@ -336,11 +363,11 @@ def main():
         # the same kernel on a workload that does NOT fit the 256 MiB Infinity
         # Cache: C2's 71 MB of input stays L3-resident across launches, C3's 1.2 GB
         # cannot -- the honest HBM fraction
-        del runner, plan
+        del runner, runners, plan
         torch.cuda.empty_cache()
         hbm = kernel_roofline(pkg, eng, args.hbm_config, args.kernel_reps, torch)
     if rank == 0 and world == 1 and not args.no_e2e and cfg in E2E_CONFIGS:
-        runner = plan = batch = None
+        runner = runners = plan = batch = None
         torch.cuda.empty_cache()
         e2e = e2e_cli(pkg, cfg)
 
@@ -356,7 +383,8 @@ def main():
                        "profile": profile, "aligned_bases_per_step": aligned,
                        "cs_bytes_gpu0": int(sum(int(s["cs_off"][-1] - s["cs_off"][0]) for s in samples)),
                        "min_depth_factor": mdf, "global_threshold_factor": gtf,
-                       "parallelism": ("replicas" if cfg == "c5" else "read-shard") + f"x{world}"},
+                       "parallelism": ("replicas" if cfg == "c5" else "read-shard") + f"x{world}",
+                       "batches_in_flight": R},
             "roofline": {"bound": "hbm", "kernel": "K_parse", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "mean_launch_us": k_ms * 1e3,

@@ -161,6 +161,26 @@ def test_repeat_launches_identical(pkg):
             _cmp(got, first, "repeat")
 
 
+def test_batches_in_flight_on_two_streams(pkg):
+    """bench.py --inflight: independent plans on two streams, steps interleaved
+    without host synchronisation, each equal to the oracle (the look-back status
+    words of concurrent launches carry different epochs)."""
+    import torch
+    syn = pkg.synth.Synth(n=2686, n_reads=6000, profile="default", seed=91, frac_partial=0.2)
+    samples = [syn.sample(0), syn.sample(1)]
+    runners = [pkg.engine.Runner(samples) for _ in range(2)]
+    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+    for k in range(8):
+        with torch.cuda.stream(streams[k % 2]):
+            runners[k % 2].step(0.1, 5.0)
+    torch.cuda.synchronize()
+    exp = [_oracle(s, 0.1, 5.0) for s in samples]
+    for r in runners:
+        r.check()
+        for s, (got, e) in enumerate(zip(r.fetch(), exp)):
+            _cmp(got, e, ("in flight", s))
+
+
 def test_capacity_replan(pkg):
     syn = pkg.synth.Synth(n=400, n_reads=500, profile="default", seed=3, frac_partial=0.5, flank=(0, 100))
     samples = [syn.sample(0)]

@@ -14,6 +14,8 @@ import torch  # noqa: E402
 
 pkg = importlib.import_module("minion-plasmid-consensus_amd")
 eng = pkg.engine
+if os.environ.get("KEXP_LIB"):
+    eng.set_library(os.path.abspath(os.environ["KEXP_LIB"]))  # variant build under test (experiments only)
 import bench  # noqa: E402
 
 cfg = sys.argv[1] if len(sys.argv) > 1 else "c2"

@@ -2067,11 +2067,7 @@ struct FlankArgs {
   const int32_t* row_base; const int32_t* lo_f; const int32_t* hiR; const int32_t* loR;
   uint32_t* rows;
   int64_t N, read_offset;
-  uint32_t* fpart;  // [blocks][2][kWinRows * 4] each block's LDS window tallies (group fold)
-  int64_t* fw0;     // [blocks][2] their first rows
-  uint32_t* fcnt;   // [groups] arrival counters (zeroed by K_clear; the last arriver resets its own)
 };
-constexpr int kFG = 16;  // K_flank blocks per window fold group
 
 // dict code of an exact-case base (flanks are upper-cased at ingest, :270):
 // h = (c >> 1) & 3 is a perfect hash A0 C1 T2 G3 on "ACTG", bit-swapped to A0 T1 C2 G3
@@ -2233,50 +2229,11 @@ __global__ __launch_bounds__(kFR) void K_flank(FlankArgs a) {
     }
   }
   __syncthreads();
-  // The hot windows are the same rows for most blocks (gap 0 / gap n of a
-  // sample): every block adding its window with device atomics put ~2 k adds
-  // on each word at C3 (34 of K_flank's 135 us).  Instead each block stores its
-  // window, and the LAST block of every group of kFG consecutive blocks folds
-  // the group's windows and adds them once (release / acquire around the
-  // arrival counter): kFG x fewer contended atomics.
-  {
-    const int64_t b = blockIdx.x, g = b / kFG;
-    const int gsz = (int)((int64_t)gridDim.x - g * kFG < kFG ? (int64_t)gridDim.x - g * kFG : kFG);
-    uint32_t* mine = a.fpart + b * 2 * kWinRows * 4;
-    for (int k = tid; k < 2 * kWinRows * 4; k += blockDim.x) {
-      const int side = k / (kWinRows * 4), q = k % (kWinRows * 4);
-      mine[k] = win[side][(q >> 2) * 5 + (q & 3)];
-    }
-    if (tid < 2) a.fw0[2 * b + tid] = s_w0[tid];
-    __threadfence();  // release this block's window before its arrival
-    __syncthreads();
-    __shared__ uint32_t s_last;
-    if (tid == 0) {
-      const uint32_t prev = atomicAdd(a.fcnt + g, 1u);
-      s_last = prev == (uint32_t)(gsz - 1);
-      if (s_last) a.fcnt[g] = 0;  // every block of the group has arrived: ready for the next launch
-    }
-    __syncthreads();
-    if (s_last) {
-      __threadfence();  // acquire the group's windows
-      for (int side = 0; side < 2; ++side)
-        for (int q = tid; q < kWinRows * 4; q += blockDim.x) {
-          uint32_t acc = 0;
-          int64_t w0 = INT64_MIN;
-          for (int j = 0; j < gsz; ++j) {
-            const int64_t bj = g * kFG + j;
-            const int64_t wj = __hip_atomic_load(a.fw0 + 2 * bj + side, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const uint32_t v = __hip_atomic_load(a.fpart + (bj * 2 + side) * kWinRows * 4 + q, __ATOMIC_RELAXED,
-                                                 __HIP_MEMORY_SCOPE_AGENT);
-            if (wj != w0) {  // another window start (a sample boundary inside the group)
-              if (acc) atomicAdd(a.rows + w0 * 4 + q, acc);
-              acc = 0;
-              w0 = wj;
-            }
-            acc += v;
-          }
-          if (acc) atomicAdd(a.rows + w0 * 4 + q, acc);
-        }
+  for (int side = 0; side < 2; ++side) {
+    const int64_t w0 = s_w0[side];
+    for (int k = tid; k < kWinRows * 4; k += blockDim.x) {
+      const uint32_t v = win[side][(k >> 2) * 5 + (k & 3)];
+      if (v) atomicAdd(a.rows + w0 * 4 + k, v);
     }
   }
   if (lerr) {
@@ -2523,7 +2480,7 @@ struct mpc_plan {
     // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
     B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
     B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_SROW, B_WPARSE, B_WBC, B_UNITS, B_RUNT,
-    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_FPART, B_FW0, B_FCNT, B_COUNT
+    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -2668,6 +2625,7 @@ static InsArgs ins_args(const mpc_plan* p, const Dev& d) {
 }
 
 static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
+  (void)p;
   FlankArgs a;
   a.status = d.status; a.sample = d.sample; a.n_of = d.n_of; a.gbase = d.gbase;
   a.tstart = d.tstart; a.i_end = d.i_end;
@@ -2675,9 +2633,6 @@ static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
   a.right_start = d.right_start; a.rsl = d.rsl; a.roff = d.roff; a.vals_out = d.vals_out; a.rpos = d.rpos;
   a.row_base = d.row_base; a.lo_f = d.lo_f; a.hiR = d.hiR; a.loR = d.loR;
   a.rows = d.rows; a.N = d.N; a.read_offset = d.read_offset;
-  a.fpart = at<uint32_t>(p, mpc_plan::B_FPART);
-  a.fw0 = at<int64_t>(p, mpc_plan::B_FW0);
-  a.fcnt = at<uint32_t>(p, mpc_plan::B_FCNT);
   return a;
 }
 
@@ -2989,12 +2944,6 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_WSUB, (int64_t)p->work_sub.size(), 4);
   set(mpc_plan::B_BKCUR, p->tally_mode == 4 ? (int64_t)p->n_parse_wg * p->nbmax : 0, 4);
   set(mpc_plan::B_WWAVE, (int64_t)p->work_wave.size(), 4);
-  {
-    const int64_t nfb = std::max<int64_t>(1, (p->N + kFR - 1) / kFR);  // K_flank blocks (flank_grid)
-    set(mpc_plan::B_FPART, nfb * 2 * kWinRows * 4, 4);
-    set(mpc_plan::B_FW0, nfb * 2, 8);
-    set(mpc_plan::B_FCNT, (nfb + kFG - 1) / kFG, 4);
-  }
   size_t o = 0;
   for (int b = 0; b < mpc_plan::B_COUNT; ++b) {
     o = (o + 255) & ~(size_t)255;
@@ -3124,7 +3073,6 @@ int mpc_parse(mpc_plan* p, void* stream) {
     add(d.maxdepth, p->S, 0u);
     add(d.ksum, 2 * p->cnt[mpc_plan::B_KSUM], 0u);  // look-back status words (epoch-tagged as well)
     add(d.bsum, 2 * p->cnt[mpc_plan::B_BSUM], 0u);
-    add(at<uint32_t>(p, mpc_plan::B_FCNT), p->cnt[mpc_plan::B_FCNT], 0u);
     add(d.M, p->runs_cap, 0u);
     add(d.runR, p->runs_cap, 0u);
     if (p->runt_dirty) add(d.runt, 16 * p->runs_cap, 0u);

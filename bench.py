@@ -183,8 +183,8 @@ def e2e_cli(pkg, cfg, reps=2):
 
 # what bounds K_parse by its counters (profiles/r03_stalls_*)
 LIMITER = ("dependency latency of the per-round chain (three dependent LDS round trips and a DPP scan per 64 "
-           "units): waves parked on s_waitcnt 47 %, VALU at 30-50 % of its measured 4-wave rate "
-           "(profiles/r03_stalls_*, profiles/r03_micro; DESIGN.md §3)")
+           "units): waves issue 36 %, wait on s_waitcnt 35 %, dependency-stalled 29 % of their cycles; VALU at "
+           "35-60 % of its measured 4-wave rate (profiles/r03_stalls_c2_final, profiles/r03_micro; DESIGN.md §3)")
 
 
 def batch_l3_resident(cfg):

@@ -2057,6 +2057,7 @@ __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
 // gaps) are tallied in LDS windows, everything else with global atomics.
 // ---------------------------------------------------------------------------
 constexpr int kFR = 512;        // reads per block (one per thread): C2's 200k reads fit one round of resident blocks
+constexpr int kFRSmall = 128;   // ... when kFR-read blocks would not give every CU one (C1: 40 -> 157 blocks)
 constexpr int kWinRows = 256;   // LDS window rows per flank side
 
 struct FlankArgs {
@@ -2085,21 +2086,22 @@ constexpr int kStageB = 16384;  // flank bytes staged in LDS per chunk (a block'
 // without a search: the starts of the block's non-empty flanks are bits of a
 // chunk bitmap with per-word prefix counts, so owner(x) = (starts <= x) - 1 in
 // the compacted list of non-empty flanks {start, row of byte 0}.
-__global__ __launch_bounds__(kFR) void K_flank(FlankArgs a) {
+template <int FR>  // reads per block (one per thread)
+__global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
   // row r, code c at word 5 r + c: consecutive rows (the bytes of one flank,
   // on consecutive lanes) fall on distinct banks
   __shared__ uint32_t win[2][kWinRows * 5];
   __shared__ __attribute__((aligned(16))) uint8_t stage[kStageB + 16];
-  __shared__ int32_t t_start[kFR], t_row[kFR], t_read[kFR];  // compacted non-empty flanks of the current side
+  __shared__ int32_t t_start[FR], t_row[FR], t_read[FR];  // compacted non-empty flanks of the current side
   __shared__ uint32_t bm[kStageB / 32];                      // flank starts in the chunk
   __shared__ int32_t wpre[kStageB / 32];                     // starts before each bitmap word (+ chunk base)
-  __shared__ int32_t s_gap[2][kFR];
+  __shared__ int32_t s_gap[2][FR];
   __shared__ int64_t s_w0[2];
-  __shared__ int32_t s_w[kFR / 64], s_nne, s_cbase;
+  __shared__ int32_t s_w[FR / 64], s_nne, s_cbase;
   if (a.status[MPC_ST_FLAGS] & (DE_CAP | DE_INTERNAL)) return;
   const int tid = threadIdx.x, l = lane(), w = tid >> 6;
-  const int64_t r0 = (int64_t)blockIdx.x * kFR;
-  const int64_t r1 = r0 + kFR < a.N ? r0 + kFR : a.N;
+  const int64_t r0 = (int64_t)blockIdx.x * FR;
+  const int64_t r1 = r0 + FR < a.N ? r0 + FR : a.N;
   const int nr = (int)(r1 - r0);
   const int64_t tot = a.status[MPC_ST_ROWS_NEEDED];
   const int64_t r = r0 + tid;
@@ -2171,7 +2173,7 @@ __global__ __launch_bounds__(kFR) void K_flank(FlankArgs a) {
       t_row[c] = (rs[side] >= 0 && rs[side] + L <= tot) ? (int32_t)rs[side] : -1;
       t_read[c] = tid;
     }
-    if (tid == kFR - 1) s_nne = wp + inc;
+    if (tid == FR - 1) s_nne = wp + inc;
     const int64_t w0 = s_w0[side];
     uint32_t* wn = win[side];
     for (int64_t c0 = 0; c0 < nb; c0 += kStageB) {  // chunks of the block's byte range
@@ -2197,15 +2199,27 @@ __global__ __launch_bounds__(kFR) void K_flank(FlankArgs a) {
         if (rel > 0 && rel < cn) atomicOr(&bm[rel >> 5], 1u << (rel & 31));
       }
       __syncthreads();
-      {  // per-word prefix of the start bits (block scan, one word per thread)
+      {  // per-word prefix of the start bits (block scan, WPT consecutive words per thread)
+        constexpr int WPT = (kStageB / 32 + FR - 1) / FR;
         const int nwd = (int)((cn + 31) >> 5);
-        const int cnt = tid < nwd ? __popc(bm[tid]) : 0;
+        int c4[WPT], cnt = 0;
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+          const int wi = tid * WPT + j;
+          c4[j] = wi < nwd ? __popc(bm[wi]) : 0;
+          cnt += c4[j];
+        }
         const int i2 = wave_scan_i32(cnt);
         if (l == 63) s_w[w] = i2;
         __syncthreads();
-        int p2 = s_cbase;
-        for (int k = 0; k < w; ++k) p2 += s_w[k];
-        if (tid < nwd) wpre[tid] = p2 + i2 - cnt;
+        int run = s_cbase + i2 - cnt;
+        for (int k = 0; k < w; ++k) run += s_w[k];
+#pragma unroll
+        for (int j = 0; j < WPT; ++j) {
+          const int wi = tid * WPT + j;
+          if (wi < nwd) wpre[wi] = run;
+          run += c4[j];
+        }
       }
       __syncthreads();
       // consecutive lanes take consecutive bytes: a flank's bytes go to
@@ -2611,7 +2625,11 @@ static void launch_left(const mpc_plan* p, const Dev& d, hipStream_t st) {
   else hipLaunchKernelGGL(K_left<kUB>, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));
 }
 static int64_t ins_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 512)); }
-static int64_t flank_grid(const mpc_plan* p) { return std::max<int64_t>(1, (p->N + kFR - 1) / kFR); }
+static int flank_reads(const mpc_plan* p) { return (p->N + kFR - 1) / kFR < 256 ? kFRSmall : kFR; }
+static int64_t flank_grid(const mpc_plan* p) {
+  const int fr = flank_reads(p);
+  return std::max<int64_t>(1, (p->N + fr - 1) / fr);
+}
 
 static InsArgs ins_args(const mpc_plan* p, const Dev& d) {
   InsArgs a;
@@ -2634,6 +2652,12 @@ static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
   a.row_base = d.row_base; a.lo_f = d.lo_f; a.hiR = d.hiR; a.loR = d.loR;
   a.rows = d.rows; a.N = d.N; a.read_offset = d.read_offset;
   return a;
+}
+static void launch_flank(const mpc_plan* p, const Dev& d, hipStream_t st) {
+  if (flank_reads(p) == kFRSmall)
+    hipLaunchKernelGGL(K_flank<kFRSmall>, dim3(flank_grid(p)), dim3(kFRSmall), 0, st, flank_args(p, d));
+  else
+    hipLaunchKernelGGL(K_flank<kFR>, dim3(flank_grid(p)), dim3(kFR), 0, st, flank_args(p, d));
 }
 
 // One launch clears every accumulator of a run (status, bitmaps, tallies, rows).
@@ -3145,7 +3169,7 @@ int mpc_rows(mpc_plan* p, void* stream) {
   hipLaunchKernelGGL(K_ins, dim3(ins_grid(p)), dim3(kUB), 0, st, ins_args(p, d));
   HIPCHK(hipGetLastError());
   p->runt_dirty = false;  // K_ins (enqueued) zeroes every run tally it maps (all runs of all gaps)
-  if (p->N > 0) hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(kFR), 0, st, flank_args(p, d));
+  if (p->N > 0) launch_flank(p, d, st);
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -3181,7 +3205,7 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
       hipLaunchKernelGGL(K_ins, dim3(ins_grid(p)), dim3(kUB), 0, st, ins_args(p, d));
       break;
     case MPC_K_FLANK:
-      hipLaunchKernelGGL(K_flank, dim3(flank_grid(p)), dim3(kFR), 0, st, flank_args(p, d));
+      launch_flank(p, d, st);
       break;
     case MPC_K_RSORT:
       hipLaunchKernelGGL(K_rsort, dim3(1), dim3(kRS), 0, st, d, (int32_t)((p->N + kRS - 1) / kRS), (int32_t)p->end_bit);

@@ -74,6 +74,8 @@ CONFIGS = {
            "(96 over 8 GPUs), sense+antisense, sample-partitioned"),
 }
 C5_PER_GPU = 12
+# CUs the parse grid is sized for when batches are in flight (bench --inflight >= 2)
+PARSE_CUS_INFLIGHT = {"c1": 128, "c2": 160, "c3": 224, "c4": 224, "c5": 224}
 PORT_SAMPLE_BASES = 2_500_000_000  # bound of the live CPU-port timing (~6 s of C at ~4e8 b/s)
 E2E_CONFIGS = ("c1", "c2", "c3", "c4", "c5")
 
@@ -240,6 +242,8 @@ def main():
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--inflight", type=int, default=2,
                     help="batches in flight (independent pipelines on their own streams, taken in turn)")
+    ap.add_argument("--parse-cus", type=int, default=None,
+                    help="CUs the parse grid is sized for with batches in flight (default: per config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--hbm-config", default="c3",
@@ -275,12 +279,17 @@ def main():
     # batches, as a sequencing run produces; every step is still one full pass
     # over one batch)
     R = max(1, args.inflight)
+    # with batches in flight the parse grid is sized for fewer CUs, so the other
+    # batch's post-parse kernels (which cannot share a CU with the parse: it holds
+    # every VGPR) run beside it; measured per config with 2 in flight
+    # (profiles/r03_experiments/parse_cus_inflight.txt, c1_parse_workgroups_inflight.txt)
+    cus = (args.parse_cus if args.parse_cus is not None else PARSE_CUS_INFLIGHT[cfg]) if R > 1 and world == 1 else 0
 
     def make_runner():
         if world > 1 and cfg != "c5":
             dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
-            return dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange())
-        return eng.Runner(samples, device=local)
+            return dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange(), parse_cus=cus)
+        return eng.Runner(samples, device=local, parse_cus=cus)
 
     runners = [make_runner() for _ in range(R)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(R - 1)]
@@ -325,6 +334,16 @@ def main():
     value = aligned * args.steps / dt
 
     # dominant kernel: K_parse, timed live with HIP events on the launch stream
+    # (on a plan whose parse grid spans every CU, like a single batch's)
+    if cus:
+        runner.step(mdf, gtf)
+        torch.cuda.synchronize()
+        runners[0].check()
+        del runners
+        runner = eng.Runner(samples, device=local)
+        runners = [runner]
+        runner.step(mdf, gtf)
+        torch.cuda.synchronize()
     plan = runner.plan
     stream = torch.cuda.current_stream()
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.kernel_reps)]
@@ -384,7 +403,7 @@ def main():
                        "cs_bytes_gpu0": int(sum(int(s["cs_off"][-1] - s["cs_off"][0]) for s in samples)),
                        "min_depth_factor": mdf, "global_threshold_factor": gtf,
                        "parallelism": ("replicas" if cfg == "c5" else "read-shard") + f"x{world}",
-                       "batches_in_flight": R},
+                       "batches_in_flight": R, "parse_cus": cus or 256},
             "roofline": {"bound": "hbm", "kernel": "K_parse", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "mean_launch_us": k_ms * 1e3,

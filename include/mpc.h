@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MPC_ABI_VERSION 6
+#define MPC_ABI_VERSION 7
 
 /* return codes */
 #define MPC_OK 0
@@ -105,6 +105,11 @@ typedef struct {
    * them) by cs BYTES instead of by read count, so no wave waits for a longer
    * neighbour at the end of the parse.  NULL: split by read count. */
   const int64_t* h_cs_off;
+  /* CUs the parse grid is sized for (0: all 256).  With several batches in
+   * flight on separate streams, a parse that leaves CUs free lets the other
+   * batches' post-parse kernels run beside it (they cannot share a CU with the
+   * parse, which holds every VGPR of the CUs it runs on). */
+  int32_t parse_cus;
 } mpc_input;
 
 typedef struct mpc_plan mpc_plan;

@@ -2785,7 +2785,8 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     // <= the resident slots (256 CUs x per_cu), so that the parse is one balanced
     // wave of workgroups (C5: 24 samples x 10 instead of x 11 = 264 > 256 slots,
     // whose 8 second-wave workgroups doubled K_parse); >= 64 reads per workgroup
-    int64_t target = 256 * per_cu;
+    const int cus = in->parse_cus > 0 && in->parse_cus < 256 ? in->parse_cus : 256;
+    int64_t target = (int64_t)cus * per_cu;
     if (const char* e = getenv("MPC_PARSE_WGS")) target = std::max<int64_t>(1, atoll(e));  // measurement override
     const int64_t wcap = wg_reads_cap(p->tally_mode);
     auto chunks = [&](int64_t ns, int64_t R) {

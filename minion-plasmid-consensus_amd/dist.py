@@ -227,7 +227,7 @@ class ShardedPileup:
     DistExchange this process holds exactly one shard (``rank`` of the group).
     """
 
-    def __init__(self, shards, devices, ex=None, row_cap=None):
+    def __init__(self, shards, devices, ex=None, row_cap=None, parse_cus=0):
         self.ex = ex or LocalExchange()
         local = len(shards)
         if isinstance(self.ex, DistExchange):
@@ -241,7 +241,7 @@ class ShardedPileup:
         n_all = self.ex.sizes(n_local)
         offs, ng = shard_layout(n_all)
         self.batches = [eng.Batch(smp, device=dev, read_offset=offs[r], n_reads_global=ng, shard=r,
-                                  n_shards=n_shards) for smp, dev, r in zip(shards, devices, ranks)]
+                                  n_shards=n_shards, parse_cus=parse_cus) for smp, dev, r in zip(shards, devices, ranks)]
         cap = row_cap or max(b.row_estimate() for b in self.batches)
         cap = self.ex.max_int([cap] * local)[0] if isinstance(self.ex, DistExchange) else cap
         self.plans = [eng.Plan(b, cap) for b in self.batches]

@@ -14,7 +14,7 @@ from . import _build
 
 LIB_PATH = _build.LIBMPC
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED = 0, 1, 2, 3
 DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL = 1, 2, 4, 8, 16, 32
 (BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_CNT, BUF_RIGHT_CNT_ALL,
@@ -74,6 +74,7 @@ class _Input(ctypes.Structure):
         ("shard", ctypes.c_int32),
         ("n_shards", ctypes.c_int32),
         ("h_cs_off", ctypes.POINTER(ctypes.c_int64)),
+        ("parse_cus", ctypes.c_int32),
     ]
 
 
@@ -195,9 +196,11 @@ class Batch:
     plasmids) concatenated, reads grouped by sample."""
 
     def __init__(self, samples, device=0, read_offset=0, n_reads_global=None, shard=0, n_shards=1,
-                 balance_bytes=True):
+                 balance_bytes=True, parse_cus=0):
         """``balance_bytes``: hand the planner the host cs offsets so the parse
-        work is split by cs bytes (mpc.h h_cs_off); False splits by read count."""
+        work is split by cs bytes (mpc.h h_cs_off); False splits by read count.
+        ``parse_cus``: CUs the parse grid is sized for (0: all; mpc.h parse_cus),
+        fewer when other batches are in flight beside this one."""
         torch = _torch()
         if not torch.cuda.is_available():
             raise MpcError("no HIP device visible (the pileup path has no CPU fallback)")
@@ -211,6 +214,7 @@ class Batch:
         self.read_offset = int(read_offset)
         self.n_reads_global = int(n_reads_global if n_reads_global is not None else self.n_reads)
         self.shard, self.n_shards = int(shard), int(n_shards)
+        self.parse_cus = int(parse_cus)
 
         def cat_bytes(key, offkey):
             bufs, offs, base = [], [], 0
@@ -272,6 +276,7 @@ class Batch:
             shard=self.shard, n_shards=self.n_shards,
             h_cs_off=(self._keep[2].ctypes.data_as(ctypes.POINTER(ctypes.c_int64)) if self.balance_bytes
                       else ctypes.POINTER(ctypes.c_int64)()),
+            parse_cus=int(self.parse_cus),
         )
 
     def row_estimate(self):
@@ -414,8 +419,8 @@ class Runner:
     """Repeated pileups over one device-resident Batch (bench / serving loop).
     The first step sizes the row buffers exactly (re-plans once if needed)."""
 
-    def __init__(self, samples, device=0, row_cap=None):
-        self.batch = Batch(samples, device=device)
+    def __init__(self, samples, device=0, row_cap=None, parse_cus=0):
+        self.batch = Batch(samples, device=device, parse_cus=parse_cus)
         self.plan = Plan(self.batch, row_cap)
         self._sized = False
 

@@ -72,6 +72,28 @@ def test_planner_geometry(pkg):
         assert info["parse_lds_bytes"] <= 160 * 1024 and info["parse_waves"] in (8, 10, 12, 16)
 
 
+def test_planner_parse_cus(pkg):
+    """mpc_input.parse_cus (bench.py with batches in flight): the parse grid is
+    one balanced wave of resident workgroups on that many CUs -- fewer
+    workgroups than the all-CU plan, same geometry otherwise, caps still held;
+    0 and out-of-range values mean all 256 CUs."""
+    g = pkg.engine.geometry
+    shapes = [([2686, 2686], [100_000, 100_000], 63 << 20), ([10_000], [1_000_000], 1200 << 20),
+              ([30_000] * 24, [10_000] * 24, 24 * 3600 * 10_000 // 100)]
+    for args in shapes:
+        full = g(*args)
+        assert g(*args, parse_cus=256) == full and g(*args, parse_cus=-3) == full
+        prev = full["parse_workgroups"]
+        for cus in (224, 160, 128):
+            info = g(*args, parse_cus=cus)
+            for k in ("tally_mode", "parse_window", "parse_waves", "reads_per_workgroup_cap"):
+                assert info[k] == full[k], (args, cus, k)
+            assert info["parse_workgroups"] <= min(prev, cus)  # one 16-wave workgroup per CU
+            assert info["max_reads_per_workgroup"] <= info["reads_per_workgroup_cap"]
+            prev = info["parse_workgroups"]
+        assert prev < full["parse_workgroups"]
+
+
 def test_planner_reference_limit(pkg):
     """The longest reference whose parse state fits LDS (tally mode 0 with the
     fewest waves; ~314 kb); one base beyond it the parse keeps that state in HBM

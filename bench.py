@@ -282,8 +282,9 @@ def main():
     # with batches in flight the parse grid is sized for fewer CUs, so the other
     # batch's post-parse kernels (which cannot share a CU with the parse: it holds
     # every VGPR) run beside it; measured per config with 2 in flight
-    # (profiles/r03_experiments/parse_cus_inflight.txt, c1_parse_workgroups_inflight.txt)
-    cus = (args.parse_cus if args.parse_cus is not None else PARSE_CUS_INFLIGHT[cfg]) if R > 1 and world == 1 else 0
+    # (profiles/r03_experiments/parse_cus_inflight.txt, c1_parse_workgroups_inflight.txt);
+    # every rank of an N-GPU run does the same (weak scaling: the same per-GPU batch)
+    cus = (args.parse_cus if args.parse_cus is not None else PARSE_CUS_INFLIGHT[cfg]) if R > 1 else 0
 
     def make_runner():
         if world > 1 and cfg != "c5":

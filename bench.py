@@ -75,7 +75,7 @@ CONFIGS = {
 }
 C5_PER_GPU = 12
 # CUs the parse grid is sized for when batches are in flight (bench --inflight >= 2)
-PARSE_CUS_INFLIGHT = {"c1": 128, "c2": 160, "c3": 224, "c4": 224, "c5": 224}
+PARSE_CUS_INFLIGHT = {"c1": 128, "c2": 160, "c3": 224, "c4": 224, "c5": 192}
 PORT_SAMPLE_BASES = 2_500_000_000  # bound of the live CPU-port timing (~6 s of C at ~4e8 b/s)
 E2E_CONFIGS = ("c1", "c2", "c3", "c4", "c5")
 

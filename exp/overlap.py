@@ -2,7 +2,7 @@
 """Batches in flight: K steps of one Runner on one stream vs K steps alternating
 over R runners (independent workspaces, same batch data) on R streams, so a
 batch's latency-bound post-parse chain can overlap the next batch's parse.
-  python3 exp/overlap.py c2 [R ...]"""
+  python3 exp/overlap.py c2 [R ...]     (PARSE_CUS=<n>: parse grid sized for n CUs)"""
 import importlib
 import os
 import sys
@@ -23,7 +23,7 @@ Rs = [int(x) for x in sys.argv[2:]] or [1, 2, 3]
 samples, _ = bench.shard_samples(pkg, cfg, 0, 1)
 K = 40
 for R in Rs:
-    runners = [eng.Runner(samples) for _ in range(R)]
+    runners = [eng.Runner(samples, parse_cus=int(os.environ.get("PARSE_CUS", "0"))) for _ in range(R)]
     streams = [torch.cuda.Stream() for _ in range(R)]
     for r, s in zip(runners, streams):
         with torch.cuda.stream(s):

@@ -189,6 +189,11 @@ LIMITER = ("dependency latency of the per-round chain (three dependent LDS round
            "35-60 % of its measured 4-wave rate (profiles/r03_stalls_c2_final, profiles/r03_micro; DESIGN.md §3)")
 
 
+# roofline.bound: what limits K_parse as measured (its HBM fraction is still
+# reported against the 8 TB/s peak): latency of the per-round dependency chain
+ROOF_BOUND = "latency"
+
+
 def batch_l3_resident(cfg):
     """Whether the kernel's input (cs + records) fits the 256 MiB Infinity Cache
     between launches: then the FETCH counters and the achieved rate include L3 hits."""
@@ -224,7 +229,7 @@ def kernel_roofline(pkg, eng, cfg, reps, torch):
             traffic = tr.get("hbm_bytes_per_launch")
     except (OSError, ValueError):
         pass
-    out = {"config": cfg, "bound": "hbm", "kernel": "K_parse", "achieved": achieved, "peak": HBM_PEAK_GBS,
+    out = {"config": cfg, "bound": ROOF_BOUND, "kernel": "K_parse", "achieved": achieved, "peak": HBM_PEAK_GBS,
            "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic, "alg_bytes_per_launch": alg,
            "mean_launch_us": k_ms * 1e3, "aligned_bases_per_launch": batch.aligned_bases,
            "input_l3_resident": batch_l3_resident(cfg), "parse_geometry": plan.info()}
@@ -244,6 +249,8 @@ def main():
                     help="batches in flight (independent pipelines on their own streams, taken in turn)")
     ap.add_argument("--parse-cus", type=int, default=None,
                     help="CUs the parse grid is sized for with batches in flight (default: per config)")
+    ap.add_argument("--dist", action="store_true",
+                    help="take the distributed path (process group + dist.DistExchange) even at WORLD_SIZE=1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--hbm-config", default="c3",
@@ -261,7 +268,11 @@ def main():
     torch.cuda.set_device(local)
     # RCCL ("nccl") over xGMI; MPC_DIST_BACKEND=gloo rehearses the N>1 path on one GPU
     backend = os.environ.get("MPC_DIST_BACKEND", "nccl")
-    if world > 1:
+    use_dist = world > 1 or args.dist
+    if use_dist:
+        os.environ.setdefault("MASTER_PORT", "29517")
+        os.environ.setdefault("RANK", str(rank))
+        os.environ.setdefault("WORLD_SIZE", str(world))
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         if backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
@@ -286,13 +297,13 @@ def main():
     # every rank of an N-GPU run does the same (weak scaling: the same per-GPU batch)
     cus = (args.parse_cus if args.parse_cus is not None else PARSE_CUS_INFLIGHT[cfg]) if R > 1 else 0
 
-    def make_runner():
-        if world > 1 and cfg != "c5":
+    def make_runner(parse_cus):
+        if use_dist and cfg != "c5":
             dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
-            return dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange(), parse_cus=cus)
-        return eng.Runner(samples, device=local, parse_cus=cus)
+            return dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange(), parse_cus=parse_cus)
+        return eng.Runner(samples, device=local, parse_cus=parse_cus)
 
-    runners = [make_runner() for _ in range(R)]
+    runners = [make_runner(cus) for _ in range(R)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(R - 1)]
     runner = runners[0]
 
@@ -303,7 +314,7 @@ def main():
     batch = runner.batch
     aligned = batch.aligned_bases
     coll_dev = "cuda" if backend == "nccl" else "cpu"
-    if world > 1:
+    if use_dist:
         t = torch.tensor([aligned], dtype=torch.int64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.SUM)
         aligned = int(t.item())
@@ -316,7 +327,7 @@ def main():
         r.check()  # data-error flags must be clear (valid synthetic input)
 
     def barrier():
-        if world > 1:
+        if use_dist:
             dist.barrier()
 
     barrier()
@@ -327,33 +338,68 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
-    if world > 1:
+    if use_dist:
         t = torch.tensor([dt], dtype=torch.float64, device=coll_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         dt = float(t.item())
     ms = dt * 1e3 / args.steps
     value = aligned * args.steps / dt
 
-    # dominant kernel: K_parse, timed live with HIP events on the launch stream
-    # (on a plan whose parse grid spans every CU, like a single batch's)
+    def kparse_ms(plan, reps, stream, beside=None):
+        """Mean K_parse launch (HIP events on its own stream); ``beside``: a step
+        of another pipeline enqueued on its stream before each launch."""
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(reps)]
+        for a, b in ev:
+            if beside is not None:
+                beside()
+            a.record(stream)
+            plan.profile_kernel(eng.K_PARSE, stream)
+            b.record(stream)
+        torch.cuda.synchronize()
+        return float(np.mean([a.elapsed_time(b) for a, b in ev]))
+
+    # K_parse on the plan that was TIMED: with batches in flight its grid is
+    # sized for `cus` CUs and the other batch's step runs beside it
+    timed_k_ms = None
+    if R > 1:
+        def other():
+            with torch.cuda.stream(streams[1]):
+                runners[1].step(mdf, gtf)
+        timed_k_ms = kparse_ms(runners[0].plan, args.kernel_reps, streams[0], other)
+        timed_geo = runners[0].plan.info()
+        for k in range(R):
+            step(k)  # leave the plans in a clean state
+        torch.cuda.synchronize()
+        for r in runners:
+            r.check()
+
+    # one batch at a time (the latency of a step) and the dominant kernel on a
+    # plan whose parse grid spans every CU, like a single batch's
+    single_ms = ms
     if cus:
-        runner.step(mdf, gtf)
-        torch.cuda.synchronize()
-        runners[0].check()
         del runners
-        runner = eng.Runner(samples, device=local)
+        runner = make_runner(0)
         runners = [runner]
-        runner.step(mdf, gtf)
+        for _ in range(max(1, args.warmup)):
+            runner.step(mdf, gtf)
         torch.cuda.synchronize()
+        runner.check()
+        barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            runner.step(mdf, gtf)
+        torch.cuda.synchronize()
+        barrier()
+        d1 = time.perf_counter() - t1
+        if use_dist:
+            t = torch.tensor([d1], dtype=torch.float64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            d1 = float(t.item())
+        single_ms = d1 * 1e3 / args.steps
     plan = runner.plan
     stream = torch.cuda.current_stream()
-    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.kernel_reps)]
-    for a, b in ev:
-        a.record(stream)
-        plan.profile_kernel(eng.K_PARSE)
-        b.record(stream)
-    torch.cuda.synchronize()
-    k_ms = float(np.mean([a.elapsed_time(b) for a, b in ev]))
+    k_ms = kparse_ms(plan, args.kernel_reps, stream)
     runner.step(mdf, gtf)  # leave the plan in a clean state
     torch.cuda.synchronize()
     for r in runners:
@@ -404,18 +450,30 @@ def main():
                        "cs_bytes_gpu0": int(sum(int(s["cs_off"][-1] - s["cs_off"][0]) for s in samples)),
                        "min_depth_factor": mdf, "global_threshold_factor": gtf,
                        "parallelism": ("replicas" if cfg == "c5" else "read-shard") + f"x{world}",
-                       "batches_in_flight": R, "parse_cus": cus or 256},
-            "roofline": {"bound": "hbm", "kernel": "K_parse", "achieved": achieved, "peak": HBM_PEAK_GBS,
+                       "batches_in_flight": R, "parse_cus": cus or 256,
+                       "process_group": backend if use_dist else None},
+            "single_batch_ms_per_step": single_ms,
+            "what": ("value = aligned bases of K steps / wall time with %d batch copies in flight on %d streams "
+                     "(pipelined throughput); single_batch_ms_per_step = the same config one batch at a time" % (R, R)
+                     if R > 1 else "value = aligned bases of K steps / wall time, one batch at a time"),
+            "roofline": {"bound": ROOF_BOUND, "kernel": "K_parse", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
                          "alg_bytes_per_launch": alg_bytes, "mean_launch_us": k_ms * 1e3,
+                         "plan": "parse grid on all 256 CUs, nothing beside it (a single batch's launch)",
                          "limiter": LIMITER, "input_l3_resident": batch_l3_resident(cfg)},
+            "roofline_timed": None if timed_k_ms is None else {
+                "bound": ROOF_BOUND, "kernel": "K_parse", "achieved": alg_bytes / (timed_k_ms * 1e-3) / 1e9,
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg_bytes / (timed_k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
+                "mean_launch_us": timed_k_ms * 1e3, "parse_workgroups": timed_geo["parse_workgroups"],
+                "plan": "the timed plan: parse grid sized for %d CUs, the other batch's step on its own stream "
+                        "beside every launch" % cus},
             "roofline_hbm": hbm,
             "cpu_baseline": cpu,
             "e2e": e2e,
         }
         line["config"]["parse_geometry"] = geo
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if use_dist:
         dist.destroy_process_group()
 
 

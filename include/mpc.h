@@ -164,12 +164,22 @@ typedef struct {
   int32_t parse_waves;             /* waves per parse workgroup */
   int32_t parse_lds_bytes;
   int32_t parse_workgroups;
-  int32_t pad_;
+  int32_t overrides;               /* MPC_OVR_* bits: a measurement override changed this plan (only in
+                                      libraries built with -DMPC_TUNING_OVERRIDES; product builds: 0) */
   int64_t max_reads_per_workgroup;
   int64_t reads_per_workgroup_cap;
   int64_t workspace_bytes;
 } mpc_plan_info;
 int mpc_plan_get_info(const mpc_plan* plan, mpc_plan_info* info);
+#define MPC_OVR_GEOMETRY 1 /* MPC_PARSE_GEOMETRY="tm,win,nw" picked the parse geometry */
+#define MPC_OVR_WGS 2      /* MPC_PARSE_WGS=k set the parse workgroup target */
+
+/* Layout of mpc_input as this library was compiled (bindings check their own
+ * struct against it, tests/test_abi.py): returns sizeof(mpc_input) and, when
+ * offsets != NULL, writes the byte offset of the first min(cap, field count)
+ * fields in declaration order into offsets[].  Field count: MPC_INPUT_FIELDS. */
+#define MPC_INPUT_FIELDS 22
+size_t mpc_input_layout(size_t* offsets, int cap);
 /* update the per-read device pointers (same shape) without re-planning */
 int mpc_plan_set_input(mpc_plan* plan, const mpc_input* in);
 

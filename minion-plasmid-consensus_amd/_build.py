@@ -47,15 +47,17 @@ def build_ingest(force=False):
     return LIBINGEST
 
 
-def build_hip(force=False, extra=()):
+def build_hip(force=False, extra=(), out=None):
+    """libmpc.so (``out``/``extra``: experiment variants, e.g. -DMPC_TUNING_OVERRIDES)."""
+    out = out or LIBMPC
     srcs = [os.path.join(CSRC, s) for s in HIP_SOURCES]
     deps = srcs + [os.path.join(CSRC, h) for h in HIP_HEADERS] + [os.path.join(INCLUDE, "mpc.h")]
-    if force or _stale(LIBMPC, deps):
+    if force or extra or _stale(out, deps):
         hipcc = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
         cmd = [hipcc, "--offload-arch=gfx950", "-O3", "-std=c++17", "-fPIC", "-shared",
-               "-I", INCLUDE, "-I", CSRC, "-o", LIBMPC] + list(extra) + srcs
+               "-I", INCLUDE, "-I", CSRC, "-o", out] + list(extra) + srcs
         subprocess.run(cmd, check=True)
-    return LIBMPC
+    return out
 
 
 def build_all(force=False):

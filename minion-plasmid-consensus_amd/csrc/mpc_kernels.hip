@@ -61,9 +61,10 @@ constexpr uint64_t kSelAgg = 1ull << 62, kSelPre = 2ull << 62, kSelTag = 0x3ffff
 // inclusive prefix, publishes its own inclusive prefix (flag 2) and returns the
 // exclusive prefixes in pre[k].  Block b's NV words are st[NV*b .. NV*b+NV-1]; a
 // predecessor counts once all its words carry this launch's tag and the same
-// flag.  Each step reads 64 x U predecessors (U per lane), so a prefix far back
-// is reached in few dependent round trips (2.8 k blocks at C5: 11 steps of 256
-// instead of 44 of 64).  Blocks are dispatched in index order, so the blocks
+// flag.  Each step reads 64 x U predecessors (U per lane).  The launches use
+// U = 1 (MPC_LOOKBACK_U, 64 per step): U = 4 (256 per step, 11 instead of 44
+// dependent steps over C5's 2.8 k blocks) measured the same within +-4 us
+// (profiles/r03_experiments/lookback_variants.txt).  Blocks are dispatched in index order, so the blocks
 // waited on are running or done; the spin is bounded anyway (DE_INTERNAL).
 template <int NV, int U>
 __device__ void lookback(uint64_t* st, int64_t b, uint64_t tag, const int32_t* own, int64_t* pre, uint32_t* flags) {
@@ -2475,6 +2476,7 @@ struct mpc_plan {
   std::vector<int32_t> h_n, h_gbase;
   int64_t N = 0, Ng = 0, G = 0, row_cap = 0, runs_cap = 0, ins_cap = 0, ovf_cap = 0;
   int32_t S = 0;
+  int32_t overrides = 0;  // MPC_OVR_* (experiment builds only)
   uint32_t sentinel = 0;
   int end_bit = 0;
   size_t ws_bytes = 0;
@@ -2686,6 +2688,19 @@ static inline unsigned nblk(int64_t n, int b = 256) {
 extern "C" {
 
 int mpc_version(void) { return MPC_ABI_VERSION; }
+
+size_t mpc_input_layout(size_t* off, int cap) {
+#define MPC_F(f) offsetof(mpc_input, f)
+  static const size_t o[] = {MPC_F(ref), MPC_F(ref_off), MPC_F(cs), MPC_F(cs_off), MPC_F(tstart), MPC_F(up),
+                             MPC_F(up_off), MPC_F(down), MPC_F(down_off), MPC_F(sample), MPC_F(n_samples),
+                             MPC_F(h_ref_len), MPC_F(h_read_begin), MPC_F(n_reads), MPC_F(cs_bytes), MPC_F(cs_base),
+                             MPC_F(read_offset), MPC_F(n_reads_global), MPC_F(shard), MPC_F(n_shards),
+                             MPC_F(h_cs_off), MPC_F(parse_cus)};
+#undef MPC_F
+  static_assert(sizeof(o) / sizeof(o[0]) == MPC_INPUT_FIELDS, "mpc_input field table");
+  for (int k = 0; off && k < cap && k < MPC_INPUT_FIELDS; ++k) off[k] = o[k];
+  return sizeof(mpc_input);
+}
 const char* mpc_last_error(void) { return g_err.c_str(); }
 
 int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
@@ -2758,7 +2773,9 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     // tuning override for measurements: MPC_PARSE_GEOMETRY="tm,win,nw" takes that
     // candidate when it fits the LDS budget (else the planner's choice)
     int o_tm = -1, o_win = -1, o_nw = -1;
+#ifdef MPC_TUNING_OVERRIDES  // experiment builds only (scripts/geom_ab.py); reported in mpc_plan_info.overrides
     if (const char* e = getenv("MPC_PARSE_GEOMETRY")) sscanf(e, "%d,%d,%d", &o_tm, &o_win, &o_nw);
+#endif
     for (const auto& c : cand)
       for (int nw : {16, 12, 8}) {
         if (c[0] == 3 && !sub_events && best > 0) break;  // global-atomic tm 3 only when nothing else fits
@@ -2767,8 +2784,12 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
         if (lds > lds_cap) continue;
         const int wgs = std::max(1, std::min(lds_cap / lds, max_waves_cu / nw));
         int score = wgs * nw * (c[1] == 512 ? 75 : c[1] == 1024 ? 95 : 100);
-        if (c[0] == o_tm && c[1] == o_win && nw == o_nw) score = 1 << 30;
-        if (score > best) { best = score; p->tally_mode = c[0]; p->parse_win = c[1]; p->parse_nw = nw; per_cu = wgs; }
+        const bool forced = c[0] == o_tm && c[1] == o_win && nw == o_nw;
+        if (forced) score = 1 << 30;
+        if (score > best) {
+          best = score; p->tally_mode = c[0]; p->parse_win = c[1]; p->parse_nw = nw; per_cu = wgs;
+          p->overrides = forced ? (p->overrides | MPC_OVR_GEOMETRY) : (p->overrides & ~MPC_OVR_GEOMETRY);
+        }
       }
     if (best < 0) {
       // references beyond every LDS mode (~312 kb): per-gap parse state in HBM
@@ -2787,7 +2808,12 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     // whose 8 second-wave workgroups doubled K_parse); >= 64 reads per workgroup
     const int cus = in->parse_cus > 0 && in->parse_cus < 256 ? in->parse_cus : 256;
     int64_t target = (int64_t)cus * per_cu;
-    if (const char* e = getenv("MPC_PARSE_WGS")) target = std::max<int64_t>(1, atoll(e));  // measurement override
+#ifdef MPC_TUNING_OVERRIDES
+    if (const char* e = getenv("MPC_PARSE_WGS")) {  // measurement override
+      target = std::max<int64_t>(1, atoll(e));
+      p->overrides |= MPC_OVR_WGS;
+    }
+#endif
     const int64_t wcap = wg_reads_cap(p->tally_mode);
     auto chunks = [&](int64_t ns, int64_t R) {
       int64_t ch = (ns + R - 1) / R;
@@ -2994,7 +3020,7 @@ int mpc_plan_get_info(const mpc_plan* p, mpc_plan_info* info) {
   info->max_reads_per_workgroup = p->max_wg_reads;
   info->reads_per_workgroup_cap = wg_reads_cap(p->tally_mode);
   info->workspace_bytes = (int64_t)p->ws_bytes;
-  info->pad_ = 0;
+  info->overrides = p->overrides;
   return MPC_OK;
 }
 

@@ -46,13 +46,13 @@ class PlanInfo(ctypes.Structure):
     """mpc_plan_info (include/mpc.h): the geometry the planner chose."""
     _fields_ = [
         ("tally_mode", ctypes.c_int32), ("parse_window", ctypes.c_int32), ("parse_waves", ctypes.c_int32),
-        ("parse_lds_bytes", ctypes.c_int32), ("parse_workgroups", ctypes.c_int32), ("pad_", ctypes.c_int32),
+        ("parse_lds_bytes", ctypes.c_int32), ("parse_workgroups", ctypes.c_int32), ("overrides", ctypes.c_int32),
         ("max_reads_per_workgroup", ctypes.c_int64), ("reads_per_workgroup_cap", ctypes.c_int64),
         ("workspace_bytes", ctypes.c_int64),
     ]
 
     def as_dict(self):
-        return {k: getattr(self, k) for k, _ in self._fields_ if k != "pad_"}
+        return {k: getattr(self, k) for k, _ in self._fields_}
 
 
 class _Input(ctypes.Structure):
@@ -81,17 +81,49 @@ class _Input(ctypes.Structure):
 _lib = None
 
 
+def _hip_runtime_paths():
+    """Distinct files of the HIP runtime (libamdhip64) mapped into this process."""
+    paths = set()
+    try:
+        with open("/proc/self/maps") as f:
+            for line in f:
+                p = line.split()[-1] if line.strip() else ""
+                if os.path.basename(p).startswith("libamdhip64.so"):
+                    paths.add(os.path.realpath(p))
+    except OSError:
+        pass
+    return paths
+
+
+def _preload_hip_runtime():
+    """libmpc.so needs libamdhip64.so.7 (its SONAME).  PyTorch-ROCm ships its own
+    copy of that library (same SONAME) with its own HSA runtime in torch/lib;
+    two HIP/HSA runtimes in one process leave the second one with "no
+    ROCm-capable device".  When PyTorch is installed, map ITS copy first
+    (RTLD_GLOBAL, by path, without importing torch): the dynamic linker then
+    binds libmpc.so's dependency to it by SONAME, and a later ``import torch``
+    finds the same file already mapped -- one runtime in either import order.
+    Without PyTorch (a C-ABI user) the system ROCm copy is used."""
+    import importlib.util
+    spec = importlib.util.find_spec("torch")
+    if spec is None or not spec.origin:
+        return
+    path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
+    if os.path.exists(path):
+        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+
+
 def lib():
     global _lib
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise MpcError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() (no CPU fallback)")
-        # libmpc.so links the system ROCm HIP/HSA runtimes while PyTorch carries
-        # its own copies: the process holds two.  Bring PyTorch's up first (the
-        # order every GPU test and the bench run in); loading libmpc.so first
-        # left its first HIP call with "no ROCm-capable device" on the MI355X box.
-        _torch().cuda.is_available()
+        _preload_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)
+        rt = _hip_runtime_paths()
+        if len(rt) > 1:
+            raise MpcError("two HIP runtimes are mapped into this process (%s): load libmpc.so through "
+                           "engine.lib() before anything else loads a HIP runtime" % ", ".join(sorted(rt)))
         vp, i64, i32, dbl = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double
         L.mpc_version.restype = i32
         L.mpc_last_error.restype = ctypes.c_char_p
@@ -102,6 +134,8 @@ def lib():
         L.mpc_plan_buffer.argtypes = [vp, i32, ctypes.POINTER(ctypes.c_size_t), ctypes.POINTER(i64)]
         L.mpc_plan_set_input.argtypes = [vp, ctypes.POINTER(_Input)]
         L.mpc_plan_get_info.argtypes = [vp, ctypes.POINTER(PlanInfo)]
+        L.mpc_input_layout.argtypes = [ctypes.POINTER(ctypes.c_size_t), i32]
+        L.mpc_input_layout.restype = ctypes.c_size_t
         for f in PHASES:
             getattr(L, "mpc_" + f).argtypes = [vp, vp]
         L.mpc_consensus.argtypes = [vp, dbl, dbl, vp]

@@ -1,7 +1,10 @@
 #!/usr/bin/env python3
 """Parse geometry A/B: the parse phase (K_clear + K_parse [+ K_subs]) and the
 full step under planner overrides (MPC_PARSE_GEOMETRY="tm,win,nw", read at plan
-creation), interleaved in one process, HIP events, medians.
+creation), interleaved in one process, HIP events, medians.  The overrides are
+compiled only into the experiment build exp/v/tuning.so (-DMPC_TUNING_OVERRIDES;
+build it first with `python3 -c "import _build; _build.build_hip(out='exp/v/tuning.so',
+extra=['-DMPC_TUNING_OVERRIDES'])"` from the package directory).
   python3 scripts/geom_ab.py c2:default,2/2048/8,1/1024/8 c3:default,3/2048/8"""
 import importlib
 import os
@@ -14,6 +17,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, REPO)
 pkg = importlib.import_module("minion-plasmid-consensus_amd")
 eng = pkg.engine
+eng.set_library(os.path.join(REPO, "exp", "v", "tuning.so"))
 bench = importlib.import_module("bench")
 
 

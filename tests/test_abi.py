@@ -3,6 +3,8 @@
 import ctypes
 import os
 import re
+import subprocess
+import sys
 
 import numpy as np
 import pytest
@@ -12,7 +14,7 @@ REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 def declared(header="mpc.h"):
     txt = open(os.path.join(REPO, "include", header)).read()
-    return sorted(set(re.findall(r"^(?:int|void|const char\*)\s+(mpc_\w+)\(", txt, re.M)))
+    return sorted(set(re.findall(r"^(?:int|void|size_t|const char\*)\s+(mpc_\w+)\(", txt, re.M)))
 
 
 def test_header_declares_entry_points():
@@ -23,8 +25,8 @@ def test_header_declares_entry_points():
 
 
 def test_library_exports_all(pkg):
-    path = pkg._build.build_hip()
-    lib = ctypes.CDLL(path)
+    pkg._build.build_hip()
+    lib = pkg.engine.lib()  # (a bare CDLL would map the system HIP runtime beside PyTorch's)
     for name in declared():
         assert hasattr(lib, name), name
     lib.mpc_version.restype = ctypes.c_int
@@ -152,3 +154,55 @@ def test_parse_split(pkg, shape):
             tot = off[b] - off[a]
             first = off[cb[nw]] - off[a]
             assert 0.45 * tot <= first <= 0.8 * tot, (first, tot)
+
+
+def _integration_fields():
+    """Field names of the mpc_input ctypes class in INTEGRATION.md's binding."""
+    txt = open(os.path.join(REPO, "INTEGRATION.md")).read()
+    m = re.search(r"class mpc_input\(ctypes\.Structure\):.*?_fields_ = \[(.*?)\n\n", txt, re.S)
+    assert m, "INTEGRATION.md has no mpc_input binding"
+    return re.findall(r'\("(\w+)",', m.group(1))
+
+
+def test_input_struct_layout(pkg):
+    """The ctypes mpc_input (engine._Input) and INTEGRATION.md's minimal binding
+    match the header as libmpc.so was compiled: size, field order, offsets."""
+    e = pkg.engine
+    L = e.lib()
+    n = len(e._Input._fields_)
+    off = (ctypes.c_size_t * n)()
+    size = L.mpc_input_layout(off, n)
+    assert size == ctypes.sizeof(e._Input)
+    assert n == 22  # MPC_INPUT_FIELDS
+    for k, (name, _) in enumerate(e._Input._fields_):
+        assert off[k] == getattr(e._Input, name).offset, name
+    assert _integration_fields() == [f for f, _ in e._Input._fields_]
+    hdr = open(os.path.join(REPO, "include", "mpc.h")).read()
+    body = re.sub(r"/\*.*?\*/", "", hdr[hdr.index("typedef struct {"):hdr.index("} mpc_input;")], flags=re.S)
+    names = re.findall(r"^\s+[\w\s\*]+?\b(\w+);", body, re.M)
+    assert names == [f for f, _ in e._Input._fields_]
+
+
+def test_plan_info_no_overrides(pkg):
+    """Product builds ignore the planners' measurement overrides:
+    the env variables change nothing and mpc_plan_info reports none."""
+    env = dict(os.environ, MPC_PARSE_GEOMETRY="2,1024,8", MPC_PARSE_WGS="3")
+    code = ("import importlib,sys; sys.path.insert(0, %r); pkg = importlib.import_module('minion-plasmid-consensus_amd'); "
+            "g = pkg.engine.geometry([2686, 2686], [100000, 100000], 63 << 20); "
+            "print(g['overrides'], g['tally_mode'], g['parse_window'], g['parse_waves'], g['parse_workgroups'])" % REPO)
+    out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, check=True).stdout.split()
+    ref = pkg.engine.geometry([2686, 2686], [100000, 100000], 63 << 20)
+    assert out == [str(x) for x in (0, ref["tally_mode"], ref["parse_window"], ref["parse_waves"], ref["parse_workgroups"])]
+
+
+@pytest.mark.parametrize("order", ["lib_first", "torch_first"])
+def test_one_hip_runtime_either_order(order):
+    """libmpc.so and PyTorch share ONE HIP runtime whichever loads first
+    (two runtimes in one process broke the first HIP call); the
+    host-only planner does not import torch."""
+    steps = {"lib_first": "e.lib(); g = e.geometry([2686], [1000], 1 << 20); t = 'torch' in sys.modules; import torch",
+             "torch_first": "import torch; t = False; e.lib()"}[order]
+    code = ("import importlib, sys; sys.path.insert(0, %r); e = importlib.import_module('minion-plasmid-consensus_amd.engine'); "
+            "%s; print(len(e._hip_runtime_paths()), t)" % (REPO, steps))
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True).stdout.split()
+    assert out == ["1", "False"], out

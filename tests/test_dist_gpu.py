@@ -114,3 +114,67 @@ def test_c3_eight_shards_in_process(pkg):
             for s, (got, f) in enumerate(zip(plan.fetch(), full)):
                 du.compare(got, du.derive(f, mdf, gtf), ("c3x8", k, s, mdf))
     del sp
+
+
+def _nccl_worker(port, q):
+    """ONE rank on cuda:0 over RCCL ("nccl"): two ShardedPileups in flight on
+    one communicator, on two streams (bench.py --dist --inflight 2 at N=1)."""
+    try:
+        os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+        import torch
+        import torch.distributed as tdist
+        torch.cuda.set_device(0)
+        tdist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+        try:
+            pkg = importlib.import_module("minion-plasmid-consensus_amd")
+            dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
+            bench = importlib.import_module("bench")
+            samples, _ = bench.shard_samples(pkg, "c2", 0, 1)
+            ex = dmod.DistExchange()
+            assert not ex.host_staged  # device tensors in place: the RCCL branches of dist.py
+            sps = [dmod.ShardedPileup([samples], [0], ex=ex) for _ in range(2)]
+            streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
+            out = []
+            for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
+                for rep in range(2):  # the second pass runs without host syncs (cached run count)
+                    for k in (0, 1):
+                        with torch.cuda.stream(streams[k]):
+                            sps[k].step(mdf, gtf)
+                torch.cuda.synchronize()
+                for k in (0, 1):
+                    sps[k].check()
+                    out.append((mdf, gtf, k, [dict(r) for r in sps[k].fetch()]))
+            q.put((out, None))
+        finally:
+            tdist.destroy_process_group()
+    except Exception as e:  # reported to the parent
+        import traceback
+        q.put((None, traceback.format_exc() + repr(e)))
+
+
+@pytest.mark.timeout(600)
+def test_rccl_world1_two_pipelines(pkg):
+    """The nccl (RCCL) branch of dist.DistExchange executed on hardware: a
+    world-size-1 process group on cuda:0 (init_process_group("nccl",
+    device_id=...)), C2 at full size (BASELINE configs[1]), two pipelines in
+    flight on one communicator.  Every call of both pipelines must equal the C
+    oracle's at full pileup and at 0.1 / 5."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    p = ctx.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    try:
+        out, err = q.get(timeout=540)
+    finally:
+        p.join(timeout=60)
+        if p.is_alive():
+            p.kill()
+    assert err is None, err
+    assert p.exitcode == 0
+    bench = importlib.import_module("bench")
+    samples, _ = bench.shard_samples(pkg, "c2", 0, 1)
+    full = du.oracle_many(samples, -1.0, 1.0)
+    assert len(out) == 4
+    for mdf, gtf, k, got in out:
+        for s, (g, f) in enumerate(zip(got, full)):
+            du.compare(g, du.derive(f, mdf, gtf), ("rccl1", k, s, mdf))

@@ -293,6 +293,32 @@ def test_long_reference(pkg, n, mode):
             _cmp(r, _oracle(s, mdf, gtf), ("long_ref", n, mdf))
 
 
+@pytest.mark.timeout(300)
+def test_long_reference_mode4_many_reads(pkg):
+    """Tally mode 4 under load: a 400 kb reference with 1,500
+    indel-heavy reads, so the parse spans many workgroups and every chunk group,
+    with thousands of insertion events per bucket placed through the HBM
+    scatter cursors (parse_epilogue_big: other waves' device atomics seen after
+    the barrier).  Bit-exact full pileup vs the oracle, and repeat launches give
+    identical calls (the order of a bucket's events may vary, the counts may not)."""
+    syn = pkg.synth.Synth(n=400_000, n_reads=1500, profile="indel", seed=49, frac_partial=0.9, antisense=False)
+    samples = [syn.sample(0)]
+    run = pkg.engine.Runner(samples)
+    info = run.plan.info()
+    assert info["tally_mode"] == 4 and info["parse_workgroups"] >= 8, info
+    exp = _oracle(samples[0], -1.0, 1.0)
+    first = None
+    for rep in range(3):
+        run.step(-1.0, 1.0)
+        run.check()
+        got = run.fetch()[0]
+        if first is None:
+            first = got
+            _cmp(got, exp, "mode4_many")
+        else:
+            _cmp(got, first, ("mode4_repeat", rep))
+
+
 def test_reference_past_coordinate_limit(pkg):
     """2^20 - 1 bases: beyond the 32-bit coordinate scheme (mpc.h), rejected."""
     long = {"ref": np.zeros((1 << 20) - 1, dtype=np.uint8) + ord("A"), "cs": np.frombuffer(b"Z::1", np.uint8).copy(),

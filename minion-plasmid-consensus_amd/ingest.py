@@ -15,7 +15,9 @@ writes nothing, like the reference).
 memory-mapped, multi-threaded, same results) and falls back to the Python
 restatement below when the native library declines an input feature it does
 not restate (non-ASCII bytes, carriage returns, integers in a form only
-Python's int() accepts) or is not built.
+Python's int() accepts) or is not built.  Non-ASCII text is transcoded to one
+byte per character with the same semantics (transcode_*: the device path is
+byte-based).
 """
 import ctypes
 import os
@@ -113,11 +115,72 @@ def read_flanks(path, recs):
     return flanks
 
 
-def _ascii(s, what):
+# Non-ASCII text (the reference decodes its files as str, :163, :196, :257):
+# the device path works on bytes, one byte per character, so every non-ASCII
+# character is transcoded to ONE byte with the same effect on the reference's
+# semantics.  A character the reference would write as a base ({A,T,C,G} dict
+# keys after .upper(), :59-61 / :70-71 / :87 / :96) and that is not one of them
+# becomes NON_BASE (a byte outside ACGT, so the device raises the same KeyError
+# if and only if it is written); coordinates count characters, as str does.
+NON_BASE = 0x80
+_SPECIAL = ":Z+-*"  # SPECIAL_CHARS (:290)
+
+
+def _base_byte(c):
+    """One byte for character c where only its .upper() as a base matters."""
+    if ord(c) < 128:
+        return c.encode("ascii")
+    u = c.upper()
+    return u.encode("ascii") if u in ("A", "C", "G", "T") else bytes((NON_BASE,))
+
+
+def transcode_ref(refseq):
+    """The upper-cased reference string (:165) -> one byte per character."""
     try:
-        return s.encode("ascii")
+        return refseq.encode("ascii")
     except UnicodeEncodeError:
-        raise IngestError(f"non-ASCII character in {what} (unsupported)") from None
+        return b"".join(_base_byte(c) for c in refseq)
+
+
+def transcode_flank(seq):
+    """An upper-cased flank (:264-265, :270) -> one byte per character: every
+    flank character is written as a base (:303, :323)."""
+    try:
+        return seq.encode("ascii")
+    except UnicodeEncodeError:
+        return b"".join(_base_byte(c) for c in seq)
+
+
+def transcode_cs(cs):
+    """A cs tag -> ASCII bytes with the same tokens (:306-320) and the same
+    effect of every operation (:74-104): a ':' operand that holds non-ASCII
+    characters is replaced by the value Python's int() gives it (Unicode
+    digits and spaces; a negative value matches nothing, like 0; a ValueError
+    stays one), '-' and 'Z' operands keep their length in characters, '*' and
+    '+' operand characters map through _base_byte."""
+    try:
+        return cs.encode("ascii")
+    except UnicodeEncodeError:
+        pass
+    out, k, n = [], 0, len(cs)
+    while k < n:
+        j = k + 1 if cs[k] in _SPECIAL else k  # operator (or none: "Unknown operator", :100)
+        e = j
+        while e < n and cs[e] not in _SPECIAL:
+            e += 1
+        op, operand = cs[k:j], cs[j:e]
+        if op == ":" and operand and not operand.isascii():
+            try:
+                v = int(operand)
+                operand = str(v) if v > 0 else "0"
+            except ValueError:
+                operand = "x"  # int() fails on the device too
+        elif op in (":", "-", "Z", ""):
+            operand = "".join(c if ord(c) < 128 else "n" for c in operand)
+        out.append(op.encode("ascii"))
+        out.append(b"".join(_base_byte(c) for c in operand) if op in ("*", "+") else operand.encode("ascii"))
+        k = e
+    return b"".join(out)
 
 
 def _concat(items):
@@ -304,16 +367,16 @@ def pack_sample_python(ref_path, paf_path, reads_path):
             raise IngestError(f"KeyError: 'upstream_seq' (read {name} not in {reads_path})")
         if t < 0 or t >= 2 ** 31:
             raise IngestError(f"target start {t} of read {name} out of range (unsupported)")
-        cs.append(_ascii(c, "cs tag"))
-        up.append(_ascii(fl[0], "read sequence"))
-        down.append(_ascii(fl[1], "read sequence"))
+        cs.append(transcode_cs(c))
+        up.append(transcode_flank(fl[0]))
+        down.append(transcode_flank(fl[1]))
         ts.append(t)
         aligned.append(qe - qs)
     cs_b, cs_off = _concat(cs)
     up_b, up_off = _concat(up)
     dn_b, dn_off = _concat(down)
     return dict(
-        ref=np.frombuffer(_ascii(refseq, "reference"), dtype=np.uint8),
+        ref=np.frombuffer(transcode_ref(refseq), dtype=np.uint8),
         cs=np.frombuffer(cs_b, dtype=np.uint8), cs_off=cs_off,
         tstart=np.asarray(ts, dtype=np.int64),
         up=np.frombuffer(up_b, dtype=np.uint8), up_off=up_off,

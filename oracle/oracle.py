@@ -16,6 +16,8 @@ import ctypes
 import os
 import subprocess
 
+import re
+
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -149,6 +151,37 @@ def format_outputs(res):
 BASE_COMPLIMENT = {"A": "T", "T": "A", "G": "C", "C": "G", "N": "N"}
 
 
+_ACGT = frozenset("ACGT")
+
+
+def _base_bytes(s):
+    """One byte per character of a str whose characters are only ever used as
+    bases (reference :184, flanks :303/:323): a non-ASCII character whose
+    .upper() is not a single A/C/G/T can never be a dict key -> 0x80."""
+    return bytes(ord(c) if ord(c) < 128 else (ord(c.upper()) if c.upper() in _ACGT else 0x80) for c in s)
+
+
+def _cs_bytes(cs):
+    """A cs tag -> bytes, one operation at a time (:306-320): ':' operands by
+    their int() value (Unicode digits; ValueError kept as one), '-' and 'Z'
+    operands by their length in characters, '*' / '+' operands as bases."""
+    if cs.isascii():
+        return cs.encode("ascii")
+    out = bytearray()
+    for op, operand in re.findall(r"([:Z+*-]?)([^:Z+*-]*)", cs):
+        out += op.encode("ascii")
+        if op == ":" and not operand.isascii():
+            try:
+                out += b"%d" % max(int(operand), 0)
+            except ValueError:
+                out += b"?"
+        elif op in ("*", "+"):
+            out += _base_bytes(operand)
+        else:
+            out += b"n" * len(operand) if not operand.isascii() else operand.encode("ascii")
+    return bytes(out)
+
+
 def ingest_files(ref_path, paf_path, reads_path):
     """Pure-Python restatement of Steps 1-3 (:161-277).  Returns the packed
     inputs of one sample, or raises KeyError/IndexError/ValueError exactly where
@@ -194,10 +227,9 @@ def ingest_files(ref_path, paf_path, reads_path):
     for r in recs:
         if "up" not in r:
             raise KeyError("upstream_seq")
-    enc = lambda s: s.encode("latin-1")
-    cs = [enc(r["cs"]) for r in recs]
-    up = [enc(r["up"]) for r in recs]
-    dn = [enc(r["down"]) for r in recs]
+    cs = [_cs_bytes(r["cs"]) for r in recs]
+    up = [_base_bytes(r["up"]) for r in recs]
+    dn = [_base_bytes(r["down"]) for r in recs]
     off = lambda xs: np.concatenate([[0], np.cumsum([len(x) for x in xs], dtype=np.int64)]).astype(np.int64)
-    return dict(ref=enc(refseq), cs=b"".join(cs), cs_off=off(cs), tstart=np.array([r["ts"] for r in recs], np.int64),
+    return dict(ref=_base_bytes(refseq), cs=b"".join(cs), cs_off=off(cs), tstart=np.array([r["ts"] for r in recs], np.int64),
                 up=b"".join(up), up_off=off(up), down=b"".join(dn), down_off=off(dn))

@@ -182,6 +182,46 @@ def hand_cases(script):
                (float("nan"), 1)], "threshold edges incl. inf/nan")
 
 
+def unicode_cases(script):
+    """Non-ASCII text: the reference reads str, so coordinates
+    count characters, str.upper() may change lengths, int() takes Unicode
+    digits, and a non-ACGT character only fails where it is written."""
+    R = ">ref\nACGTACGTAC\n"
+    one = lambda cs, qlen=10, qs=0, qe=10, ts=0, te=10: paf_line("r1", qlen, qs, qe, "+", ts, te, cs)
+    # reference: non-ASCII where no read writes (uncovered tail) -> fine; 'ß'.upper() == 'SS' shifts coordinates
+    emit_case(script, "u_ref_tail", ">ref \u00e9t\u00e9\nACGTACGTAC\u00e9\u00df\u4e2d\n", ">r1\nACGTACGTAC\n",
+              one(":10"), [(0, 1), (-1, 1)], "non-ASCII reference characters no read covers")
+    emit_case(script, "u_ref_sharp_s", ">ref\nAC\u00dfGTACGT\n", ">r1\nGTACGT\n",
+              one(":6", qlen=6, qs=0, qe=6, ts=4, te=10), [(0, 1), (-1, 1)], "upper() lengthens the reference")
+    emit_case(script, "u_ref_matched", ">ref\nACGT\u00e9CGTAC\n", ">r1\nACGTACGTAC\n", one(":10"), [(0, 1)],
+              "a matched non-ASCII reference base: KeyError")
+    emit_case(script, "u_ref_subbed", ">ref\nACGT\u00e9CGTAC\n", ">r1\nACGTACGTAC\n", one(":4*\u00e9a:5"),
+              [(0, 1), (-1, 1)], "a substituted non-ASCII reference base is never written")
+    # cs operands
+    emit_case(script, "u_del_operand", R, ">r1\nACGTCGTAC\n", one(":3-\u00e9:6", qlen=9, qe=9), [(0, 1), (-1, 1)],
+              "deletion of a non-ASCII character counts one")
+    emit_case(script, "u_del_cjk", R, ">r1\nACGTAC\n", one(":2-\u4e2d\u00fc\u00e9\u00df:4", qlen=6, qe=6), [(0, 1), (-1, 1)],
+              "deletion operand of 4 non-ASCII characters")
+    emit_case(script, "u_colon_fullwidth", R, ">r1\nACGTTCGTAC\n", one(":\uff14*at:\uff15"), [(0, 1), (-1, 1)],
+              "int() of fullwidth digits")
+    emit_case(script, "u_colon_arabic", R, ">r1\nACGTACGTAC\n", one(":\u0661\u0660"), [(0, 1)],
+              "int() of Arabic-Indic digits (10)")
+    emit_case(script, "u_colon_bad", R, ">r1\nACGTACGTAC\n", one(":1\u00e9"), [(0, 1)], "int() ValueError")
+    emit_case(script, "u_sub_first", R, ">r1\nACGTTCGTAC\n", one(":4*\u00e9t:5"), [(0, 1), (-1, 1)],
+              "only operand[-1] of '*' is written")
+    emit_case(script, "u_sub_last", R, ">r1\nACGTTCGTAC\n", one(":4*a\u00e9:5"), [(0, 1)], "KeyError")
+    emit_case(script, "u_ins", R, ">r1\nACGTTTCGTAC\n", one(":4+\u00e9:6", qlen=11, qe=11), [(0, 1)], "KeyError")
+    emit_case(script, "u_z_operand", R, ">r1\nACGTACGTAC\n", one(":4Z\u00e9\u00e9:6"), [(0, 1), (-1, 1)],
+              "'Z' ignores its operand")
+    # reads: names, aligned part (never written), flanks (written)
+    emit_case(script, "u_read_name", R, ">r\u00e9 x\nACGTACGTAC\n",
+              paf_line("r\u00e9 x", 10, 0, 10, "+", 0, 10, ":10"), [(0, 1)], "non-ASCII read name")
+    emit_case(script, "u_read_aligned", R, ">r1\nGGACGT\u00e9\u00dfCGTACTT\n",
+              one(":10", qlen=16, qs=2, qe=13), [(0, 1), (-1, 1)], "non-ASCII inside the aligned part; 'ß' -> 'SS'")
+    emit_case(script, "u_flank", R, ">r1\n\u00e9ACGTACGTAC\n", one(":10", qlen=11, qs=1, qe=11), [(0, 1)],
+              "non-ASCII upstream flank base: KeyError")
+
+
 def random_cases(script):
     specs = [
         # name, n, reads, profile, seed, frac_partial, flank, ins_len, del_len
@@ -211,9 +251,14 @@ def random_cases(script):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref-script", default="/root/reference/src/mapped_paf_read_parser.py")
+    ap.add_argument("--only", default="", help="'unicode': regenerate only the non-ASCII cases")
     a = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
+    if a.only == "unicode":
+        unicode_cases(a.ref_script)
+        return
     hand_cases(a.ref_script)
+    unicode_cases(a.ref_script)
     random_cases(a.ref_script)
 
 

@@ -45,7 +45,8 @@ def _same(ing, ref, paf, reads, expect_native=True):
 @pytest.mark.parametrize("case", gu.cases())
 def test_golden_inputs(ing, case, tmp_path):
     ref, reads, paf = gu.materialize(case, str(tmp_path))
-    _same(ing, ref, paf, reads, expect_native="crlf" not in case)
+    # the native parser declines CR line ends and non-ASCII text (u_*: Python path)
+    _same(ing, ref, paf, reads, expect_native="crlf" not in case and not case.startswith("u_"))
 
 
 @pytest.mark.parametrize("spec", [

@@ -974,6 +974,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       // the read's slot (tstart, read, i_end), loaded before the decode; its
       // base s_val is read after this round's read starts have written theirs
       const int32_t q_ts = W.s_ts[q], q_read = W.s_read[q], q_iend = W.s_iend[q];
+#ifdef MPC_ABL_NODECODE  // timing ablation only (wrong results): no decode
+      int adv0 = 0, adv = (s0 & 7) == 0 ? 1 : 0, kind = v ? 2 : 0, olen_e = 2;
+      uint32_t pay = (uint32_t)s0 & 3u, err = 0;
+#else
       // fast decode from the staged bytes: op, then 4 operand bytes
       const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage);
       const int a4 = sx >> 2;
@@ -1039,6 +1043,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
           err |= tp.err;
         }
       }
+#endif
       MPC_SEG(2);
       // ---- coordinates ----
       const int advu = adv0 + adv;            // unit advance <= 2^21: 64 lanes stay < 2^31
@@ -1060,7 +1065,11 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
                          ((kind == 2) & ((uint32_t)i >= (uint32_t)n)) | ((kind == 3) & ((uint32_t)i > (uint32_t)n));
       uint32_t te = err | (bad_i ? DE_INDEX : 0u);
       const int rl = q_read;
+#ifdef MPC_ABL_NOEFFECTS  // timing ablation only (wrong results): no tallies / events
+      const bool ok = false;
+#else
       const bool ok = te == 0;
+#endif
       if (ok & (kind == 2) & (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
       const bool del = ok & (kind == 4) & (i >= 0) & (i < n);
       if (del) {
@@ -1070,7 +1079,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if (ok & (kind == 3)) left_bit(i);
       if (ok & (kind == 3) & (olen_e > kInsInline)) push_ovf(a, A + sx + 1, rl, i, olen_e);
       if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window
-        const bool sev = te == 0 && kind == 2;
+        const bool sev = ok && kind == 2;
         const int win = i >> kSubWinBits;
         uint16_t* wp = a.subev + sev_base;  // window ww's region of this wave
         for (int ww = 0; ww < a.sub_wins; ++ww, wp += a.subev_cap) {
@@ -1082,7 +1091,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
           if (l == ww) nsub_v += (uint32_t)__popcll(bw);
         }
       }
-      const bool ins_inline = kind == 3 && olen_e <= kInsInline && te == 0;
+      const bool ins_inline = kind == 3 && olen_e <= kInsInline && ok;
       const uint64_t bins = ballot(ins_inline);
       if (ins_inline) {
         a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);

@@ -1,4 +1,5 @@
 #!/bin/bash
+set -o pipefail
 # Round-4 GPU check: parity suite (incl. the RCCL world-1 test), default bench,
 # and bench.py's distributed branch under torchrun at WORLD_SIZE=1 (RCCL).
 R=${GRAFT_REPO_ROOT:-$(pwd)}

@@ -130,6 +130,7 @@ def run_case(name, script, core, repeats=1, golden=True):
     frac = (b - a) / full
     return cfg, {
         "value": aligned / wall, "unit": "aligned bases/s", "cores": 1, "kind": "reference",
+        "value_best": aligned / ws[0], "wall_min_s": round(ws[0], 3),
         "wall_s": round(wall, 3), "walls_s": [round(w, 3) for w in walls], "repeats": len(walls),
         "spread": round((ws[-1] - ws[0]) / wall, 4),
         "aligned_bases": aligned, "strand_jobs": strands,
@@ -142,12 +143,57 @@ def run_case(name, script, core, repeats=1, golden=True):
     }
 
 
+def run_all_cores(script, cores, repeats, reads=1000):
+    """BASELINE configs[4] on ALL host cores: the 96-plasmid batch
+    is independent jobs, so the reference runs as one process per core, each on
+    its own plasmid (the bench's C5 seeds 5000 + k, reads [0, reads) of 10k, both
+    strands one after the other), started together; throughput = all aligned
+    bases / wall of the slowest.  ``repeats`` batches, median and min recorded."""
+    kw = dict(n=30_000, n_reads=10_000, profile="default", antisense=True)
+    env = dict(os.environ, PYTHONDONTWRITEBYTECODE="1")
+    walls, aligned = [], 0
+    with tempfile.TemporaryDirectory() as tmp:
+        jobs = []
+        for k, core in enumerate(cores):
+            syn = synth.Synth(reads=(0, reads), seed=5000 + k, **kw)
+            aligned += int(sum(int(syn.sample(s)["aligned"].sum()) for s in range(2)))
+            d = os.path.join(tmp, f"p{k}")
+            os.makedirs(d)
+            syn.write_files(*(os.path.join(d, f) for f in ("ref.fa", "reads.fa", "s0.paf", "ref1.fa", "s1.paf")))
+            sh = " && ".join(
+                f"taskset -c {core} {sys.executable} -B {script} --ref {d}/{ref} --reads {d}/reads.fa --paf {d}/s{s}.paf "
+                f"--consensus {d}/c{s}.fa --chromat {d}/ch{s}.tsv --accuracies {d}/acc{s}.tsv "
+                f"--min_depth_factor 0.1 --global_threshold_factor 5.0 > /dev/null"
+                for s, ref in ((0, "ref.fa"), (1, "ref1.fa")))
+            jobs.append(sh)
+        for rep in range(repeats):
+            t0 = time.perf_counter()
+            procs = [subprocess.Popen(["bash", "-c", j], env=env) for j in jobs]
+            rcs = [p.wait() for p in procs]
+            wall = time.perf_counter() - t0
+            if any(rcs):
+                raise SystemExit(f"c5 all-cores: reference exit {rcs}")
+            walls.append(wall)
+            print(f"c5 all cores rep{rep}: {wall:.2f} s", flush=True)
+    ws = sorted(walls)
+    wall = ws[len(ws) // 2]
+    return {"value": aligned / wall, "value_best": aligned / ws[0], "unit": "aligned bases/s", "cores": len(cores),
+            "kind": "reference", "wall_s": round(wall, 3), "wall_min_s": round(ws[0], 3),
+            "walls_s": [round(w, 3) for w in walls], "repeats": len(walls), "spread": round((ws[-1] - ws[0]) / wall, 4),
+            "aligned_bases": aligned, "extrapolated": True,
+            "sample": (f"c5 on all {len(cores)} host cores: {len(cores)} reference processes started together, one per "
+                       f"core (taskset), each one plasmid (seeds 5000..{4999 + len(cores)}) with reads [0, {reads}) of "
+                       f"its 10k and both strand jobs one after the other; median of {len(walls)} batch(es); rate "
+                       "extrapolated linearly to the full set (SURVEY §8(d))")}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref-script", default="/root/reference/src/mapped_paf_read_parser.py")
     ap.add_argument("--core", type=int, default=0)
     ap.add_argument("--only", nargs="*")
-    ap.add_argument("--repeats", type=int, default=3, help="timed repetitions per case (median recorded)")
+    ap.add_argument("--repeats", type=int, default=5, help="timed repetitions per case (median and min recorded)")
+    ap.add_argument("--all-cores", action="store_true", help="only the C5 all-host-cores throughput (configs.c5_all_cores)")
     ap.add_argument("--no-golden", action="store_true", help="time only; leave tests/golden_depth untouched")
     a = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
@@ -155,6 +201,13 @@ def main():
     rec["host"] = {"cpu_model": cpu_model(), "logical_cpus": os.cpu_count(), "python": platform.python_version(),
                    "where": "build container (the reference does not exist on the GPU box)"}
     rec.setdefault("configs", {})
+    if a.all_cores:
+        r = run_all_cores(a.ref_script, list(range(os.cpu_count() or 1)), a.repeats)
+        rec["configs"]["c5_all_cores"] = r
+        with open(RECORD, "w") as f:
+            json.dump(rec, f, indent=1, sort_keys=True)
+        print(json.dumps({"c5_all_cores": r}), flush=True)
+        return
     for name in a.only or CASES:
         cfg, r = run_case(name, a.ref_script, a.core, a.repeats, not a.no_golden)
         rec["configs"][cfg] = r

@@ -17,3 +17,9 @@ def pytest_configure(config):
 @pytest.fixture(scope="session")
 def pkg():
     return importlib.import_module("minion-plasmid-consensus_amd")
+
+
+# experiments only: MPC_TEST_LIB=exp/v/<variant>.so runs the suite against a
+# variant build of libmpc.so (engine.set_library, before anything loads it)
+if os.environ.get("MPC_TEST_LIB"):
+    importlib.import_module("minion-plasmid-consensus_amd").engine.set_library(os.path.abspath(os.environ["MPC_TEST_LIB"]))

@@ -297,13 +297,18 @@ def main():
     # every rank of an N-GPU run does the same (weak scaling: the same per-GPU batch)
     cus = (args.parse_cus if args.parse_cus is not None else PARSE_CUS_INFLIGHT[cfg]) if R > 1 else 0
 
-    def make_runner(parse_cus):
+    # one communicator per pipeline in flight (every rank creates them in the
+    # same order): a pipeline's collectives then run on their own RCCL stream
+    # instead of queueing behind the other pipeline's on one shared stream
+    groups = [dist.new_group(list(range(world))) for _ in range(R)] if use_dist and cfg != "c5" else [None] * R
+
+    def make_runner(parse_cus, group=None):
         if use_dist and cfg != "c5":
             dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
-            return dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange(), parse_cus=parse_cus)
+            return dmod.ShardedPileup([samples], [local], ex=dmod.DistExchange(group), parse_cus=parse_cus)
         return eng.Runner(samples, device=local, parse_cus=parse_cus)
 
-    runners = [make_runner(cus) for _ in range(R)]
+    runners = [make_runner(cus, groups[k]) for k in range(R)]
     streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(R - 1)]
     runner = runners[0]
 
@@ -378,7 +383,7 @@ def main():
     single_ms = ms
     if cus:
         del runners
-        runner = make_runner(0)
+        runner = make_runner(0, groups[0])
         runners = [runner]
         for _ in range(max(1, args.warmup)):
             runner.step(mdf, gtf)

@@ -85,10 +85,10 @@ typedef struct {
   const int32_t* sample;   /* [n_reads] sample id */
   /* ---- host-side sizes ---- */
   int32_t n_samples;
-  const int64_t* h_ref_len;    /* host [n_samples] reference lengths n_s (0 <= n_s <= 1048574 = 2^20 - 2: 32-bit
-                                  coordinates with the advance clamp; up to ~312 kb the parse keeps its per-gap
-                                  state in LDS, beyond it in HBM (tally mode 4); mpc_plan_create fails with
-                                  MPC_E_ARG past 2^20 - 2) */
+  const int64_t* h_ref_len;    /* host [n_samples] reference lengths n_s (0 <= n_s <= 4194302 = 2^22 - 2: 32-bit
+                                  coordinates with the advance clamp, 22-bit gaps in the insertion events; up
+                                  to ~312 kb the parse keeps its per-gap state in LDS, beyond it in HBM (tally
+                                  mode 4); mpc_plan_create fails with MPC_E_ARG past 2^22 - 2) */
   const int64_t* h_read_begin; /* host [n_samples+1] local reads of sample s: [h_read_begin[s], h_read_begin[s+1]) */
   int64_t n_reads;             /* local reads */
   int64_t cs_bytes;            /* cs_off[n_reads] - cs_off[0] */

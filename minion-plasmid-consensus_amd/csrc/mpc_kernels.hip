@@ -44,8 +44,13 @@ constexpr uint32_t DE_OP = MPC_DE_OP, DE_VALUE = MPC_DE_VALUE, DE_INDEX = MPC_DE
 
 constexpr int kBlk = 1024;          // cs bytes staged per wave iteration (64 lanes x 16 B)
 constexpr int kInsInline = 4;       // insertions up to this length travel as one event word
-constexpr int kMaxRefLen = (1 << 20) - 2;  // 32-bit coordinates: advances are clamped at kAdvCap > n
-constexpr int kAdvCap = 1 << 20;    // > any reference length: a clamped advance keeps i past the end
+// 32-bit coordinates: a unit's advances are clamped at kAdvCap > n (a clamped
+// advance still leaves i past the end); a window's prefix of advances then
+// stays below (WIN / 8) * 2^23 (a ':' operand worth 2^22 takes >= 8 bytes) and
+// every coordinate below kICap + 2^30 + 2^29 < 2^31.  The insertion event word
+// holds the gap in 22 bits (kNullGap).
+constexpr int kMaxRefLen = (1 << 22) - 2;
+constexpr int kAdvCap = 1 << 22;    // > any reference length: a clamped advance keeps i past the end
 constexpr int kICap = 1 << 28;      // saturation of the running coordinate i
 constexpr int kBW = 64;             // gaps per insertion bucket (K_left workgroup)
 static_assert(kBW <= 64 && (kBW & (kBW - 1)) == 0, "sorted insertion events hold the gap within its bucket in 6 bits");
@@ -263,14 +268,22 @@ constexpr int kMaxCh = MPC_PARSE_CHUNKS;  // read chunks per parse workgroup, ta
 // would hold more (LDS budget), smaller windows never hold more than WIN
 template <int WIN> constexpr int tok_cap() { return WIN <= 1024 ? WIN : 1024; }
 
+// K_parse stages a window's cs bytes by LDS-DMA (global_load_lds_dwordx4,
+// no VGPRs) into the other of two per-wave stage buffers while the current
+// window's rounds run (windows of 1-2 KiB; 512-byte windows load into VGPRs)
+#ifndef MPC_PARSE_DMA
+#define MPC_PARSE_DMA 1
+#endif
+template <int WIN> constexpr bool parse_dma() { return MPC_PARSE_DMA && WIN >= 1024; }
+template <int WIN> constexpr int stage_bufs() { return parse_dma<WIN>() ? 2 : 1; }
+
 template <int WIN>
 struct alignas(16) WaveLds {            // per-wave LDS of K_parse
-  int32_t s_val[kSlots];                // i = s_val + (window prefix of advances)
   int32_t s_ts[kSlots];                 // tstart (clamped; -1: negative)
   int32_t s_read[kSlots];               // local read index
   int32_t s_iend[kSlots];               // i_end | bit 30: read has a downstream flank
   int64_t s_end[kSlots];                // cs offset of the read's end
-  uint8_t stage[WIN + 16];              // window bytes (+16: word reads past the end)
+  uint8_t stage[stage_bufs<WIN>()][WIN + 16];  // window bytes (+16: word reads past the end)
   uint8_t em[WIN / 8];                  // boundary bits (special characters | read starts), bit = byte
   uint8_t ra[WIN / 8];                  // read-start bits
   uint16_t tok[tok_cap<WIN>() + 2 + 64];  // unit starts in [P, C), then the sentinel C; bits 12-14: ':' prefix
@@ -407,7 +420,9 @@ __device__ __forceinline__ int lanes_below(uint64_t m) {
 
 // Per-byte character classes of a lane's staged bytes, SWAR per 32-bit word
 // (no per-byte compares: those pin 2 SGPRs per byte): bit k of sp = byte k is
-// special (: Z * + -), of cm = ':', of om = an op ('*', '+', '-').
+// special (: Z * + -), of cm = ':'.  The ops that may follow a ':' prefix in
+// one unit are sp & ~cm ('Z' included: a unit ':n' + 'Z' decodes as the two
+// tokens it is, so only two masks are compacted per word).
 __device__ __forceinline__ uint32_t byte_hits(uint32_t w, uint32_t pat) {  // bit 7 of byte k: byte k == pat's
   const uint32_t t = w ^ pat;
   return ~(((t & 0x7F7F7F7Fu) + 0x7F7F7F7Fu) | t) & 0x80808080u;
@@ -418,34 +433,42 @@ __device__ __forceinline__ uint32_t hit_nibble(uint32_t z) {  // bits 7, 15, 23,
   z |= z >> 14;
   return z & 0xfu;
 }
+// Special bytes by two v_perm table lookups per word: a byte c = (hi, lo) is
+// special iff lo >= 8, c < 0x80 and bit hi of T1[lo & 7] is set -- T1[2] (lo
+// 0xA) = {2, 3, 5} for '*' ':' 'Z', T1[3] (lo 0xB) = {2} for '+', T1[5] (lo
+// 0xD) = {2} for '-' -- i.e. T1[lo & 7] & (1 << hi) != 0, the second lookup
+// giving 1 << (hi & 7).  That AND is 8 exactly for ':' (hi 3), so both masks
+// come from one pair of lookups.
 template <int NW>
-__device__ __forceinline__ void word_classes(const uint32_t* w, uint32_t* sp, uint32_t* cm, uint32_t* om) {
-  uint32_t s_ = 0, c_ = 0, o_ = 0;
+__device__ __forceinline__ void word_classes(const uint32_t* w, uint32_t* sp, uint32_t* cm) {
+  uint32_t s_ = 0, c_ = 0;
 #pragma unroll
   for (int i = 0; i < NW; ++i) {
-    const uint32_t zc = byte_hits(w[i], 0x3A3A3A3Au);
-    const uint32_t zo = byte_hits(w[i] & 0xFEFEFEFEu, 0x2A2A2A2Au) | byte_hits(w[i], 0x2D2D2D2Du);  // * + | -
-    const uint32_t zs = zc | zo | byte_hits(w[i], 0x5A5A5A5Au);
+    const uint32_t c = w[i];
+    const uint32_t t1 = __builtin_amdgcn_perm(0x00000400u, 0x042C0000u, c & 0x07070707u);
+    const uint32_t t2 = __builtin_amdgcn_perm(0x80402010u, 0x08040201u, (c >> 4) & 0x07070707u);
+    const uint32_t y = t1 & t2;                   // per byte: 0, or the single bit 1 << hi (<= 0x20)
+    const uint32_t ok = (c << 4) & ~c;            // bit 7 of a byte: lo >= 8 and c < 0x80
+    const uint32_t zs = (y + 0x7F7F7F7Fu) & ok & 0x80808080u;  // bit 7: y != 0 (no carry out: y <= 0x20)
+    const uint32_t zc = (y << 4) & ok & 0x80808080u;           // bit 7: y == 8 (':')
     s_ |= hit_nibble(zs) << (4 * i);
     c_ |= hit_nibble(zc) << (4 * i);
-    o_ |= hit_nibble(zo) << (4 * i);
   }
   *sp = s_;
   *cm = c_;
-  *om = o_;
 }
 struct alignas(16) U8x32 { uint4 a, b; };  // a lane's 32 bytes of a 2 KiB window
-__device__ __forceinline__ void chunk_classes(uint2 v, uint32_t* sp, uint32_t* cm, uint32_t* om) {
+__device__ __forceinline__ void chunk_classes(uint2 v, uint32_t* sp, uint32_t* cm) {
   const uint32_t w[2] = {v.x, v.y};
-  word_classes<2>(w, sp, cm, om);
+  word_classes<2>(w, sp, cm);
 }
-__device__ __forceinline__ void chunk_classes(uint4 v, uint32_t* sp, uint32_t* cm, uint32_t* om) {
+__device__ __forceinline__ void chunk_classes(uint4 v, uint32_t* sp, uint32_t* cm) {
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  word_classes<4>(w, sp, cm, om);
+  word_classes<4>(w, sp, cm);
 }
-__device__ __forceinline__ void chunk_classes(U8x32 v, uint32_t* sp, uint32_t* cm, uint32_t* om) {
+__device__ __forceinline__ void chunk_classes(U8x32 v, uint32_t* sp, uint32_t* cm) {
   const uint32_t w[8] = {v.a.x, v.a.y, v.a.z, v.a.w, v.b.x, v.b.y, v.b.z, v.b.w};
-  word_classes<8>(w, sp, cm, om);
+  word_classes<8>(w, sp, cm);
 }
 // bits [0, x) set, x in [0, 32]
 __device__ __forceinline__ uint32_t lowmask(int x) { return x >= 32 ? 0xffffffffu : (1u << x) - 1u; }
@@ -484,11 +507,11 @@ struct WinIn {
   uint32_t uo, dno;  // low words of the flank offsets: only the lengths' signs are needed
   int32_t ts;
 };
-template <int CH>
+template <int CH, bool DATA = true>
 __device__ __forceinline__ WinIn<CH> fetch_window(const ParseArgs& a, int64_t P, int64_t rs0, int l) {
   WinIn<CH> f;
   const int64_t A = P & ~(int64_t)15;
-  f.d = *reinterpret_cast<const typename Chunk<CH>::T*>(a.cs + A + CH * l);
+  if (DATA) f.d = *reinterpret_cast<const typename Chunk<CH>::T*>(a.cs + A + CH * l);
   const int64_t r = rs0 + l;
   const bool ok = r <= a.n_reads;
   f.o = ok ? a.cs_off[r] : INT64_MAX;
@@ -496,6 +519,27 @@ __device__ __forceinline__ WinIn<CH> fetch_window(const ParseArgs& a, int64_t P,
   f.dno = ok ? reinterpret_cast<const uint32_t*>(a.down_off)[2 * r] : 0u;
   f.ts = r < a.n_reads ? a.tstart[r] : 0;
   return f;
+}
+// 1 KiB of global memory at src (16 B per lane) into LDS at dst (wave-uniform
+// byte address), by LDS-DMA: no VGPR destination; the hardware counts it on
+// vmcnt, the compiler does not (the consumer waits vmcnt(0) itself).  M0 is
+// written and restored inside the one statement (cdna_hip_programming.md).
+__device__ __forceinline__ void dma_1k(const uint8_t* src, uint32_t dst) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep) : "v"(src + 16 * lane()), "s"(dst) : "memory");
+}
+template <int WIN>
+__device__ __forceinline__ void dma_window(const uint8_t* src, uint8_t* stage) {
+  const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(uintptr_t)stage);
+#pragma unroll
+  for (int k = 0; k < WIN / 1024; ++k) dma_1k(src + 1024 * k, dst + 1024u * k);
+}
+__device__ __forceinline__ void chunk_load(const uint8_t* p, uint4& v) { v = *reinterpret_cast<const uint4*>(p); }
+__device__ __forceinline__ void chunk_load(const uint8_t* p, uint2& v) { v = *reinterpret_cast<const uint2*>(p); }
+__device__ __forceinline__ void chunk_load(const uint8_t* p, U8x32& v) {
+  v.a = reinterpret_cast<const uint4*>(p)[0];
+  v.b = reinterpret_cast<const uint4*>(p)[1];
 }
 __device__ __forceinline__ void chunk_store(uint8_t* p, uint4 v) { *reinterpret_cast<uint4*>(p) = v; }
 __device__ __forceinline__ void chunk_store(uint8_t* p, uint2 v) { *reinterpret_cast<uint2*>(p) = v; }
@@ -788,7 +832,11 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   uint32_t nev = 0;                                       // events written (wave-uniform)
   int64_t rs0 = ra;         // first read whose cs starts at or after P
   bool carry = false;       // slot 0 holds a read continuing into this window
-  WinIn<CH> cur = fetch_window<CH>(a, P, rs0, l);
+  int32_t c_base = 0;       // ... and its coordinate base (wave-uniform): i = base + window prefix of advances
+  constexpr bool dma = parse_dma<WIN>();
+  int sb = 0;               // stage buffer of the current window
+  if (dma && P < wend) dma_window<WIN>(a.cs + (P & ~(int64_t)15), W.stage[0]);
+  WinIn<CH> cur = fetch_window<CH, !dma>(a, P, rs0, l);
   while (P < wend) {
     const int64_t A = P & ~(int64_t)15;
     // ---- window: at most 63 read starts in [P, E) ----
@@ -806,13 +854,19 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         a.i_end[rs0 + l] = cur.ts < 0 ? 0 : (cur.ts > n ? n + 1 : cur.ts);
       }
       rs0 += 63;
-      cur = fetch_window<CH>(a, P, rs0, l);
+      cur = fetch_window<CH, !dma>(a, P, rs0, l);  // (same P: the staged bytes stay)
       continue;
     }
     // ---- stage bytes, boundary bits ----
-    chunk_store(W.stage + CH * l, cur.d);
-    uint32_t spm, cm_own, om_own;
-    chunk_classes(cur.d, &spm, &cm_own, &om_own);
+    if (dma) {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // this window's LDS-DMA has landed
+      chunk_load(W.stage[sb] + CH * l, cur.d);
+    } else {
+      chunk_store(W.stage[0] + CH * l, cur.d);
+    }
+    uint32_t spm, cm_own;
+    chunk_classes(cur.d, &spm, &cm_own);
+    const uint32_t om_own = spm & ~cm_own;
     put_lane_bits<CH>(W.em, l, spm);
     put_lane_bits<CH>(W.ra, l, 0u);
     wave_sync_lds();
@@ -895,10 +949,11 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       W.s_read[q] = (int32_t)(rs0 + l);
       W.s_iend[q] = (ts < 0 ? 0 : (ts > n ? n + 1 : ts)) | (dn ? 1 << 30 : 0);
     }
-    // ---- the next window starts at C (its loads are issued after this
-    // window's rounds: holding them across the rounds cost 12 VGPRs and bought
-    // nothing, the other 15 waves hide the latency) ----
+    // ---- the next window starts at C: its bytes go by LDS-DMA into the other
+    // stage buffer now, behind this window's rounds (its read records load
+    // after the rounds: holding them across the rounds costs VGPRs) ----
     const int64_t Pn = C, rsn = rs0 + nst;
+    if (dma && Pn < wend) dma_window<WIN>(a.cs + (Pn & ~(int64_t)15), W.stage[sb ^ 1]);
     // ---- token list: starts in [P, C) (bit 15 = read start), then the sentinel ----
     int T;
     {
@@ -907,32 +962,37 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       thi = thi < 0 ? 0 : (thi > CH ? CH : thi);
       const uint32_t rng = lowmask(thi) & ~lowmask(tlo);
       const uint32_t tm = em_own & rng;
-      // Units: a ':' token with 1-4 operand bytes and the op token ('*', '+',
-      // '-') right after it in the same read, both in [P, C), are ONE list
-      // entry (bits 12-14: the ':' operand length); every other token is its
-      // own entry.  Bit-parallel over this lane's bytes and the 5 bytes either
-      // side (DPP wave shifts): bit 5 + k of a neighbourhood mask = own byte k.
+      // Units: a ':' token with 1-4 operand bytes and the op token right after
+      // it in the same read, both in [P, C), are ONE list entry (bits 12-14: the
+      // ':' operand length); every other token is its own entry.  Bit-parallel
+      // on 32-bit masks: bit k of at(m, d) = bit k + d of this lane's mask m
+      // continued by the next lane's, so a ':' at k has operand length d - 1
+      // when the first boundary after it is an op at k + d (d = 2..5).
       const uint32_t cmr = cm_own & rng, omr = om_own & ~ra_own & rng;
-      auto hood = [&](uint32_t x, bool below, bool above) {
-        uint64_t h = (uint64_t)x << 5;
-        if (below) h |= (uint64_t)((from_lane_below(x) >> (CH - 5)) & 31u);
-        if (above) h |= (uint64_t)(from_lane_above(x) & 31u) << (CH + 5);
-        return h;
+      const uint32_t em_nx = from_lane_above(em_own), om_nx = from_lane_above(omr);
+      auto at = [&](uint32_t own, uint32_t nx, int d) -> uint32_t {
+        if constexpr (CH == 32) return __builtin_amdgcn_alignbit(nx, own, (uint32_t)d);
+        else return (own | (nx << CH)) >> d;
       };
-      const uint64_t em3 = hood(em_own, true, true), cm3 = hood(cmr, true, true), om3 = hood(omr, false, true);
-      const uint64_t nb1 = ~(em3 << 1), nb12 = nb1 & ~(em3 << 2), nb123 = nb12 & ~(em3 << 3);
-      const uint64_t c2 = (cm3 << 2) & nb1;                   // ':' 2 bytes before, no boundary between
-      const uint64_t c3 = (cm3 << 3) & nb12;
-      const uint64_t c4 = (cm3 << 4) & nb123;
-      const uint64_t c5 = (cm3 << 5) & nb123 & ~(em3 << 4);
-      const uint64_t ab = om3 & (c2 | c3 | c4 | c5);          // absorbed ops
-      const uint32_t own = lowmask(CH);
-      const uint32_t p2 = (uint32_t)((ab & c2) >> 7) & own;  // ':' whose op is 2 bytes on
-      const uint32_t p3 = (uint32_t)((ab & c3) >> 8) & own;
-      const uint32_t p4 = (uint32_t)((ab & c4) >> 9) & own;
-      const uint32_t p5 = (uint32_t)((ab & c5) >> 10) & own;
-      const uint32_t pl0 = p2 | p4, pl1 = p3 | p4;            // operand length d - 1 in 3 bit planes
-      const uint32_t tu = tm & ~((uint32_t)(ab >> 5) & own);
+      const uint32_t n1 = ~at(em_own, em_nx, 1), n2 = n1 & ~at(em_own, em_nx, 2);
+      const uint32_t n3 = n2 & ~at(em_own, em_nx, 3), n4 = n3 & ~at(em_own, em_nx, 4);
+      const uint32_t p2 = cmr & n1 & at(omr, om_nx, 2);  // ':' whose op is 2 bytes on
+      const uint32_t p3 = cmr & n2 & at(omr, om_nx, 3);
+      const uint32_t p4 = cmr & n3 & at(omr, om_nx, 4);
+      const uint32_t p5 = cmr & n4 & at(omr, om_nx, 5);
+      const uint32_t pl0 = p2 | p4, pl1 = p3 | p4;        // operand length d - 1 in 3 bit planes
+      // the absorbed ops: here, or (carried) in the next lane
+      uint32_t ab_own, ab_hi;
+      if constexpr (CH == 32) {
+        ab_own = (p2 << 2) | (p3 << 3) | (p4 << 4) | (p5 << 5);
+        ab_hi = (p2 >> 30) | (p3 >> 29) | (p4 >> 28) | (p5 >> 27);
+      } else {
+        const uint32_t ab = (p2 << 2) | (p3 << 3) | (p4 << 4) | (p5 << 5);
+        ab_own = ab & lowmask(CH);
+        ab_hi = ab >> CH;
+      }
+      ab_own |= from_lane_below(ab_hi);
+      const uint32_t tu = tm & ~ab_own;
       const int cnt = __popc(tu);
       const int incl = wave_scan_i32(cnt);
       T = wave_last_i32(incl);
@@ -954,6 +1014,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     const int far_c = (int)(C - A < (1 << 30) ? C - A : (1 << 30));  // wave-uniform
     int32_t G = 0;  // advances of the window's earlier rounds
     int qc = 0;     // read starts of the window's earlier rounds
+    int32_t cb = c_base;  // coordinate base of the open read (wave-uniform)
     for (int t0 = 0; t0 < T; t0 += 64) {
       const int t = t0 + l;
       const bool v = t < T;
@@ -971,98 +1032,161 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const bool last = v && (e1 >> 15);
       const uint64_t brs = ballot(is_rs);
       const int q = qc + lanes_below(brs) + (is_rs ? 1 : 0);
-      // the read's slot (tstart, read, i_end), loaded before the decode; its
-      // base s_val is read after this round's read starts have written theirs
+      // the read's slot (tstart, read, i_end), loaded before the decode
       const int32_t q_ts = W.s_ts[q], q_read = W.s_read[q], q_iend = W.s_iend[q];
 #ifdef MPC_ABL_NODECODE  // timing ablation only (wrong results): no decode
       int adv0 = 0, adv = (s0 & 7) == 0 ? 1 : 0, kind = v ? 2 : 0, olen_e = 2;
       uint32_t pay = (uint32_t)s0 & 3u, err = 0;
 #else
-      // fast decode from the staged bytes: op, then 4 operand bytes
-      const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage);
-      const int a4 = sx >> 2;
-      const uint32_t sh = (uint32_t)(sx & 3);
-      const uint32_t d0 = b32[a4], d1 = b32[a4 + 1], d2 = b32[a4 + 2];
-      const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
-      const uint32_t x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
-      const uint32_t op = x0 & 0xffu;
-      const uint32_t w0 = __builtin_amdgcn_alignbyte(x1, x0, 1u);
-      const int olen = ex - sx - 1;
-      // branch-free decode: op class, 4 operand bytes at once (SWAR)
-      const bool colon = op == ':', star = op == '*', plus = op == '+', minus = op == '-';
-      const bool spec = colon | star | plus | minus | (op == 'Z');
-      const bool act = v & spec & ((olen > 0) | last);  // empty operand: skipped unless last (:309, :320)
-      const int ol4 = olen < 0 ? 0 : (olen > 4 ? 4 : olen);
-      const uint32_t vm = ol4 == 4 ? 0xffffffffu : ((1u << (8 * ol4)) - 1u);  // operand bytes in w0
-      //   the unit's ':' operand -- its prefix (pl bytes after s0) or the main
-      //   token's own operand -- up to 4 digits: right-align, SWAR decimal
-      const bool pre = pl != 0;
-      const int pa = (s0 + 1) >> 2;
-      const uint32_t pw = __builtin_amdgcn_alignbyte(b32[pa + 1], b32[pa], (uint32_t)((s0 + 1) & 3));
-      const int cl = pre ? pl : (colon ? ol4 : 0);
-      const uint32_t cw = pre ? pw : w0;
-      const uint32_t cvm = cl == 4 ? 0xffffffffu : ((1u << (8 * cl)) - 1u);
-      const uint32_t Tx = cw ^ 0x30303030u;
-      const bool cdig = ((((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u & cvm) == 0;
-      uint32_t X = cl == 0 ? 0u : (Tx & cvm & 0x0F0F0F0Fu) << (8 * (4 - cl));
-      X = mul2561(X) >> 8;
-      X = ((X & 0x00FF00FFu) * 6553601u) >> 16;
-      const int adv_c = (int)(X & 0xffffu);
-      int adv0 = pre ? adv_c : 0;
-      const bool dig_ok = (olen >= 1) & (olen <= 4) & cdig;  // main ':' token
-      //   bases: (c|0x20) must equal "acgt"[h] with h = (lc>>1)&3 (v_perm table lookup)
-      const uint32_t lc = w0 | 0x20202020u;
-      const uint32_t hh = (lc >> 1) & 0x03030303u;
-      const uint32_t bad = lc ^ __builtin_amdgcn_perm(0u, 0x67746361u, hh);
-      const uint32_t codes = ((hh & 0x01010101u) << 1) | ((hh >> 1) & 0x01010101u);  // dict order A0 T1 C2 G3
-      const int shl = 8 * ((olen - 1) & 3);
-      const bool last_ok = ((bad >> shl) & 0xffu) == 0;  // '*': written base = operand[-1] (:96)
-      uint32_t pk = codes;
-      pk = (pk | (pk >> 6)) & 0x000f000fu;
-      pk = (pk | (pk >> 12)) & 0xffu;
-      const uint32_t mstar = 0u - (uint32_t)star;
-      uint32_t pay = (mstar & ((codes >> shl) & 3u)) | (~mstar & (pk & ((1u << (2 * ol4)) - 1u)));
-      const bool slow = lfar | (pre & !cdig) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));
-      const int kop = ((int)star << 1) | ((int)plus * 3) | ((int)minus << 2);  // exclusive classes
-      const int mcol = -(int)colon;
-      int kind = (-(int)act) & ((mcol & (int)(adv_c > 0)) | (~mcol & (-(int)(olen > 0) & kop)));
-      int adv = (-(int)(kind == 1) & adv_c) | (int)(kind == 2) | (-(int)(kind == 4) & (olen < kAdvCap ? olen : kAdvCap));
-      uint32_t err = (v & !spec) ? DE_OP : 0u;  // cs does not start with an operator (:100-102)
-      if (act & star & (olen == 0)) err |= DE_INDEX;  // operand[-1] of '' (:96)
-      if ((kind == 2) & !last_ok) err |= DE_KEY;
-      if ((kind == 3) & ((bad & vm) != 0)) err |= DE_KEY;
-      int olen_e = olen;
-      if (slow) {  // rare: decode from HBM
-        const int64_t s = A + sx, e = A + (lfar ? C - A : (int64_t)(e1 & 0xfffu));
-        const TokInfo ti = analyze_long(a.cs, s, e, last);
-        adv = ti.adv; kind = ti.kind; pay = ti.pay; err = ti.err;
-        olen_e = (int)(e - s - 1 < kAdvCap ? e - s - 1 : kAdvCap);
-        if (pl) {
-          const TokInfo tp = analyze_long(a.cs, A + s0, s, false);
-          adv0 = tp.adv;
-          err |= tp.err;
+      // ---- decode.  Fast path: every unit of the round is canonical -- an
+      // optional absorbed ':' prefix of 1-4 digits, then ':' + 1-4 digits, '*' +
+      // 1-4 bytes ending in a base, '+' + 1-4 bases or '-' + 1-4 bytes, ending
+      // inside the window -- so no data error can arise but the coordinate
+      // checks; branch-free from two 8-byte LDS reads.  A round holding any
+      // other unit ('Z', empty / long operands, non-digits, non-bases, a token
+      // past the window, a read not starting with an operator) takes the
+      // general decode below for all its lanes.
+      const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage[sb]);
+      int adv0, adv, kind, olen_e;
+      uint32_t pay, err = 0u;
+      bool fast;
+      {
+        const uint32_t sh = (uint32_t)(sx & 3);
+        uint32_t m0 = b32[sx >> 2], m1 = b32[(sx >> 2) + 1];  // bytes sx .. sx + 4 (sh + 4 <= 7)
+        const int pa = (s0 + 1) >> 2;
+        uint32_t p0 = b32[pa], p1 = b32[pa + 1];
+        // (opaque: both 8-byte reads issue together, unconditionally -- the
+        // compiler would otherwise sink the prefix read into a branch on pl)
+        asm volatile("" : "+v"(m0), "+v"(m1), "+v"(p0), "+v"(p1));
+        const uint32_t op = __builtin_amdgcn_alignbyte(m1, m0, sh) & 0xffu;
+        const uint32_t ow = sh == 3u ? m1 : __builtin_amdgcn_alignbyte(m1, m0, sh + 1u);  // operand bytes
+        const uint32_t pw = __builtin_amdgcn_alignbyte(p1, p0, (uint32_t)((s0 + 1) & 3));  // ':' prefix
+        const int olen = ex32 - sx - 1;
+        const int ol4 = olen < 0 ? 0 : (olen > 4 ? 4 : olen);
+        const bool colon = op == ':', star = op == '*', plus = op == '+', minus = op == '-';
+        const int cl = pl ? pl : (colon ? ol4 : 0);  // digits of the unit's ':' operand
+        const uint32_t cw = pl ? pw : ow;
+        const uint32_t cvm = cl == 4 ? 0xffffffffu : ((1u << (8 * cl)) - 1u);
+        const uint32_t Tx = cw ^ 0x30303030u;
+        const bool dig = ((((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u & cvm) == 0;
+        uint32_t X = (Tx & cvm & 0x0F0F0F0Fu) << ((32 - 8 * cl) & 31);  // right-aligned digits (cl = 0: 0)
+        X = mul2561(X) >> 8;
+        X = ((X & 0x00FF00FFu) * 6553601u) >> 16;
+        const int val = (int)(X & 0xffffu);
+        //   bases: (c|0x20) must equal "acgt"[h] with h = (lc>>1)&3 (v_perm table lookup)
+        const uint32_t lc = ow | 0x20202020u;
+        const uint32_t hh = (lc >> 1) & 0x03030303u;
+        const uint32_t bad = lc ^ __builtin_amdgcn_perm(0u, 0x67746361u, hh);
+        const uint32_t codes = ((hh & 0x01010101u) << 1) | ((hh >> 1) & 0x01010101u);  // dict order A0 T1 C2 G3
+        const uint32_t shl = 8u * (uint32_t)((ol4 - 1) & 3);
+        const uint32_t vm = ol4 == 4 ? 0xffffffffu : ((1u << (8 * ol4)) - 1u);
+        uint32_t pk = (codes | (codes >> 6)) & 0x000f000fu;
+        pk = (pk | (pk >> 12)) & ((1u << (2 * ol4)) - 1u);
+        fast = !v | (!lfar & (olen >= 1) & (olen <= 4) & dig &
+                     (colon | minus | (star & (((bad >> shl) & 0xffu) == 0u)) | (plus & ((bad & vm) == 0u))));
+        // branch-free: '*' 0x2A -> 2, '+' 0x2B -> 3, '-' 0x2D -> 4 from op & 7;
+        // ':' -> 1 when it matches at least one base (:77)
+        const int mv = -(int)v, mc = -(int)colon;
+        const int o7 = (int)(op & 7u);
+        kind = mv & ((mc & (int)(val > 0)) | (~mc & (o7 - (o7 >> 2))));
+        adv = mv & ((mc & val) | (int)star | (-(int)minus & ol4));
+        adv0 = mv & (-(int)(pl != 0)) & val;
+        const uint32_t ms = 0u - (uint32_t)star;
+        pay = (ms & ((codes >> shl) & 3u)) | (~ms & pk);
+        olen_e = ol4;
+      }
+      if (ballot(!fast)) {  // general decode of the whole round
+        const int a4 = sx >> 2;
+        const uint32_t sh = (uint32_t)(sx & 3);
+        const uint32_t d0 = b32[a4], d1 = b32[a4 + 1], d2 = b32[a4 + 2];
+        const uint32_t x0 = __builtin_amdgcn_alignbyte(d1, d0, sh);
+        const uint32_t x1 = __builtin_amdgcn_alignbyte(d2, d1, sh);
+        const uint32_t op = x0 & 0xffu;
+        const uint32_t w0 = __builtin_amdgcn_alignbyte(x1, x0, 1u);
+        const int olen = ex - sx - 1;
+        // branch-free decode: op class, 4 operand bytes at once (SWAR)
+        const bool colon = op == ':', star = op == '*', plus = op == '+', minus = op == '-';
+        const bool spec = colon | star | plus | minus | (op == 'Z');
+        const bool act = v & spec & ((olen > 0) | last);  // empty operand: skipped unless last (:309, :320)
+        const int ol4 = olen < 0 ? 0 : (olen > 4 ? 4 : olen);
+        const uint32_t vm = ol4 == 4 ? 0xffffffffu : ((1u << (8 * ol4)) - 1u);  // operand bytes in w0
+        //   the unit's ':' operand -- its prefix (pl bytes after s0) or the main
+        //   token's own operand -- up to 4 digits: right-align, SWAR decimal
+        const bool pre = pl != 0;
+        const int pa = (s0 + 1) >> 2;
+        const uint32_t pw = __builtin_amdgcn_alignbyte(b32[pa + 1], b32[pa], (uint32_t)((s0 + 1) & 3));
+        const int cl = pre ? pl : (colon ? ol4 : 0);
+        const uint32_t cw = pre ? pw : w0;
+        const uint32_t cvm = cl == 4 ? 0xffffffffu : ((1u << (8 * cl)) - 1u);
+        const uint32_t Tx = cw ^ 0x30303030u;
+        const bool cdig = ((((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u & cvm) == 0;
+        uint32_t X = cl == 0 ? 0u : (Tx & cvm & 0x0F0F0F0Fu) << (8 * (4 - cl));
+        X = mul2561(X) >> 8;
+        X = ((X & 0x00FF00FFu) * 6553601u) >> 16;
+        const int adv_c = (int)(X & 0xffffu);
+        adv0 = pre ? adv_c : 0;
+        const bool dig_ok = (olen >= 1) & (olen <= 4) & cdig;  // main ':' token
+        //   bases: (c|0x20) must equal "acgt"[h] with h = (lc>>1)&3 (v_perm table lookup)
+        const uint32_t lc = w0 | 0x20202020u;
+        const uint32_t hh = (lc >> 1) & 0x03030303u;
+        const uint32_t bad = lc ^ __builtin_amdgcn_perm(0u, 0x67746361u, hh);
+        const uint32_t codes = ((hh & 0x01010101u) << 1) | ((hh >> 1) & 0x01010101u);  // dict order A0 T1 C2 G3
+        const int shl = 8 * ((olen - 1) & 3);
+        const bool last_ok = ((bad >> shl) & 0xffu) == 0;  // '*': written base = operand[-1] (:96)
+        uint32_t pk = codes;
+        pk = (pk | (pk >> 6)) & 0x000f000fu;
+        pk = (pk | (pk >> 12)) & 0xffu;
+        const uint32_t mstar = 0u - (uint32_t)star;
+        pay = (mstar & ((codes >> shl) & 3u)) | (~mstar & (pk & ((1u << (2 * ol4)) - 1u)));
+        const bool slow = lfar | (pre & !cdig) | (act & ((colon & !dig_ok) | ((star | plus) & (olen > 4))));
+        const int kop = ((int)star << 1) | ((int)plus * 3) | ((int)minus << 2);  // exclusive classes
+        const int mcol = -(int)colon;
+        kind = (-(int)act) & ((mcol & (int)(adv_c > 0)) | (~mcol & (-(int)(olen > 0) & kop)));
+        adv = (-(int)(kind == 1) & adv_c) | (int)(kind == 2) | (-(int)(kind == 4) & (olen < kAdvCap ? olen : kAdvCap));
+        err = (v & !spec) ? DE_OP : 0u;  // cs does not start with an operator (:100-102)
+        if (act & star & (olen == 0)) err |= DE_INDEX;  // operand[-1] of '' (:96)
+        if ((kind == 2) & !last_ok) err |= DE_KEY;
+        if ((kind == 3) & ((bad & vm) != 0)) err |= DE_KEY;
+        olen_e = olen;
+        if (slow) {  // rare: decode from HBM
+          const int64_t s = A + sx, e = A + (lfar ? C - A : (int64_t)(e1 & 0xfffu));
+          const TokInfo ti = analyze_long(a.cs, s, e, last);
+          adv = ti.adv; kind = ti.kind; pay = ti.pay; err = ti.err;
+          olen_e = (int)(e - s - 1 < kAdvCap ? e - s - 1 : kAdvCap);
+          if (pl) {
+            const TokInfo tp = analyze_long(a.cs, A + s0, s, false);
+            adv0 = tp.adv;
+            err |= tp.err;
+          }
         }
       }
 #endif
       MPC_SEG(2);
       // ---- coordinates ----
-      const int advu = adv0 + adv;            // unit advance <= 2^21: 64 lanes stay < 2^31
+      const int advu = adv0 + adv;            // unit advance <= 2^23: 64 lanes stay < 2^29
       const int ainc = wave_scan_i32(advu);
       const int aex = ainc - advu;
       const int atot = wave_last_i32(ainc);
-      // a read starting in this round writes its base (tstart - advances before
-      // it) into its slot; every lane then reads its read's base back (one LDS
-      // round trip: fewer instructions than a DPP max-scan over the start
-      // lanes, and the parse is issue-bound): i = base + advances before the unit
-      if (is_rs) W.s_val[q] = q_ts - (G + aex);  // for later rounds and the window carry
-      wave_sync_lds();
-      const int iu = W.s_val[q] + G + aex;  // coordinate at the unit start
+      // read bases, i = base + G + aex: lanes before the round's first read
+      // start continue the open read (base cb); a read starting at lane j has
+      // base tstart - (G + aex_j) on lanes j.. up to the next start.  One
+      // scalar pass over the start lanes (about one per round: reads hold tens
+      // to hundreds of units) instead of an LDS write, fence and read back
+      int bv = cb;
+      for (uint64_t m = brs; m; m &= m - 1) {
+        const int j = __ffsll((unsigned long long)m) - 1;
+        cb = __builtin_amdgcn_readlane(q_ts, j) - (G + __builtin_amdgcn_readlane(aex, j));
+        bv = l >= j ? cb : bv;
+      }
+      const int iu = bv + G + aex;  // coordinate at the unit start
       const int i = iu + adv0;                // ... and at its main token
       MPC_SEG(3);
       // ---- effects ----
       // data errors and effects as flat predicates (no nested exec-mask regions)
-      const bool bad_i = ((adv0 > 0) & ((iu < 0) | (i > n))) | ((kind == 1) & ((i < 0) | (i + adv > n))) |
-                         ((kind == 2) & ((uint32_t)i >= (uint32_t)n)) | ((kind == 3) & ((uint32_t)i > (uint32_t)n));
+      // IndexError (refarr / obsarr past the end): a ':' prefix writes [iu, i),
+      // ':' [i, i + adv), '*' [i, i + 1), '+' the gap i: every kind 1-3 needs
+      // 0 <= i and i + adv <= n (adv = 1 for '*', 0 for '+'); sign of an OR
+      const bool bad_i = ((adv0 > 0) & ((iu | (n - i)) < 0)) | (((uint32_t)(kind - 1) <= 2u) & ((i | (n - adv - i)) < 0));
       uint32_t te = err | (bad_i ? DE_INDEX : 0u);
       const int rl = q_read;
 #ifdef MPC_ABL_NOEFFECTS  // timing ablation only (wrong results): no tallies / events
@@ -1117,9 +1241,11 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     // ---- reads that ended in this window: i_end; carry the open one ----
     if (l <= nst && (l > 0 || carry) && W.s_end[l] <= C) a.i_end[W.s_read[l]] = W.s_iend[l] & ~(1 << 30);
     const bool cont = (nst > 0 || carry) && W.s_end[nst] > C;
+    if (cont) {
+      const int64_t v = (int64_t)cb + G;
+      c_base = (int32_t)(v > kICap ? kICap : v);
+    }
     if (cont && l == 0) {
-      const int64_t v = (int64_t)W.s_val[nst] + G;
-      W.s_val[0] = (int32_t)(v > kICap ? kICap : v);
       W.s_end[0] = W.s_end[nst];
       W.s_ts[0] = W.s_ts[nst];
       W.s_read[0] = W.s_read[nst];
@@ -1129,7 +1255,8 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     wave_sync_lds();
     P = Pn;
     rs0 = rsn;
-    if (Pn < wend) cur = fetch_window<CH>(a, Pn, rsn, l);
+    sb ^= dma ? 1 : 0;
+    if (Pn < wend) cur = fetch_window<CH, !dma>(a, Pn, rsn, l);
     MPC_SEG(5);
   }
   // reads starting at the range end have an empty cs
@@ -1142,6 +1269,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   if (TM == 3 && l < a.sub_wins) a.subev_cnt[((int64_t)blockIdx.x * kMaxCh + chk) * kMaxSubWins + l] = nsub_v;
   }  // chunks
   MPC_SEG(5);
+  // every LDS-DMA was waited for by the window after it (one is issued only
+  // when another window follows); drain anyway before the LDS is reused
+  if (parse_dma<WIN>()) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   MPC_SEG(6);
   if constexpr (big) parse_epilogue_big(a, n, nbk, r0, wcnt, wbase, nch);
@@ -2733,7 +2863,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   p->h_gbase.resize(p->S + 1);
   int64_t g = 0;
   for (int s = 0; s < p->S; ++s) {
-    if (p->ref_len[s] < 0 || p->ref_len[s] > kMaxRefLen) { delete p; return fail(MPC_E_ARG, "reference length out of range (at most 2^20 - 2 bases)"); }
+    if (p->ref_len[s] < 0 || p->ref_len[s] > kMaxRefLen) { delete p; return fail(MPC_E_ARG, "reference length out of range (at most 2^22 - 2 bases)"); }
     p->h_n[s] = (int32_t)p->ref_len[s];
     p->h_gbase[s] = (int32_t)g;
     g += p->ref_len[s] + 1;

@@ -99,8 +99,8 @@ def test_planner_parse_cus(pkg):
 def test_planner_reference_limit(pkg):
     """The longest reference whose parse state fits LDS (tally mode 0 with the
     fewest waves; ~314 kb); one base beyond it the parse keeps that state in HBM
-    (tally mode 4), up to the 32-bit coordinates' 2^20 - 2 (mpc.h); past that
-    mpc_plan_create fails (host-only)."""
+    (tally mode 4), up to 2^22 - 2 (mpc.h: 32-bit coordinates, 22-bit event
+    gaps); past that mpc_plan_create fails (host-only)."""
     g = pkg.engine.geometry
     lo, hi = 100_000, 1_000_000  # bisect the last LDS-state length
     while hi - lo > 1:
@@ -114,10 +114,10 @@ def test_planner_reference_limit(pkg):
     assert info["tally_mode"] == 0 and info["parse_lds_bytes"] <= 160 * 1024
     big = g([lo + 1], [12], (lo + 1) * 3)
     assert big["tally_mode"] == 4 and big["parse_lds_bytes"] <= 160 * 1024
-    top = g([(1 << 20) - 2], [12], (1 << 20) * 3)
+    top = g([(1 << 22) - 2], [12], (1 << 22) * 3)
     assert top["tally_mode"] == 4
     with pytest.raises(pkg.engine.MpcError):
-        g([(1 << 20) - 1], [12], (1 << 20) * 3)
+        g([(1 << 22) - 1], [12], (1 << 22) * 3)
 
 
 @pytest.mark.parametrize("shape", [

@@ -275,14 +275,14 @@ def test_dense_tokens_match_oracle(pkg, seed):
         _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("dense", seed, mdf))
 
 
-@pytest.mark.parametrize("n,mode", [(300_000, 0), (400_000, 4)])
-def test_long_reference(pkg, n, mode):
-    """A 300 kb reference (parse state in LDS, tally mode 0) and a 400 kb one
-    past the LDS budget (tally mode 4: LEFT bitmap, insertion-bucket counters
-    and event-sort cursors in HBM): bit-exact full pileup and at the pipeline's
-    thresholds, against the oracle (the reference takes any length,
-    mapped_paf_read_parser.py:161-184)."""
-    syn = pkg.synth.Synth(n=n, n_reads=40, profile="default", seed=48, frac_partial=0.5, antisense=True)
+@pytest.mark.parametrize("n,mode,reads", [(300_000, 0, 40), (400_000, 4, 40), (1_500_000, 4, 16)])
+def test_long_reference(pkg, n, mode, reads):
+    """A 300 kb reference (parse state in LDS, tally mode 0), a 400 kb one past
+    the LDS budget (tally mode 4: LEFT bitmap, insertion-bucket counters and
+    event-sort cursors in HBM) and a 1.5 Mb one (coordinates past 2^20):
+    bit-exact full pileup and at the pipeline's thresholds, against the
+    oracle (the reference takes any length, mapped_paf_read_parser.py:161-184)."""
+    syn = pkg.synth.Synth(n=n, n_reads=reads, profile="default", seed=48, frac_partial=0.5, antisense=True)
     samples = [syn.sample(0), syn.sample(1)]
     assert len(samples[0]["ref"]) == n
     plan = pkg.engine.Plan(pkg.engine.Batch(samples))
@@ -320,8 +320,8 @@ def test_long_reference_mode4_many_reads(pkg):
 
 
 def test_reference_past_coordinate_limit(pkg):
-    """2^20 - 1 bases: beyond the 32-bit coordinate scheme (mpc.h), rejected."""
-    long = {"ref": np.zeros((1 << 20) - 1, dtype=np.uint8) + ord("A"), "cs": np.frombuffer(b"Z::1", np.uint8).copy(),
+    """2^22 - 1 bases: beyond the coordinate scheme (mpc.h), rejected."""
+    long = {"ref": np.zeros((1 << 22) - 1, dtype=np.uint8) + ord("A"), "cs": np.frombuffer(b"Z::1", np.uint8).copy(),
             "cs_off": np.array([0, 4], np.int64), "tstart": np.array([0], np.int64),
             "up": np.zeros(0, np.uint8), "up_off": np.zeros(2, np.int64), "down": np.zeros(0, np.uint8),
             "down_off": np.zeros(2, np.int64)}

@@ -24,9 +24,11 @@
 #include <sys/mman.h>
 #include <sys/stat.h>
 #include <unistd.h>
+#include <emmintrin.h>
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -34,7 +36,7 @@
 #include <string>
 #include <string_view>
 #include <thread>
-#include <unordered_map>
+#include <memory>
 #include <vector>
 
 namespace {
@@ -78,6 +80,17 @@ inline char upper(char c) { return (c >= 'a' && c <= 'z') ? (char)(c - 32) : c; 
 
 using mpc_host::host_threads;
 
+// MPC_INGEST_TIMING=1: wall time of each ingest phase on stderr (a measurement
+// aid; called from the launching thread only).  phase(nullptr) starts the clock.
+void phase(const char* what) {
+  static const bool on = getenv("MPC_INGEST_TIMING") != nullptr;
+  static std::chrono::steady_clock::time_point prev;
+  if (!on) return;
+  const auto t = std::chrono::steady_clock::now();
+  if (what) fprintf(stderr, "ingest %-16s %8.1f ms\n", what, std::chrono::duration<double, std::milli>(t - prev).count());
+  prev = t;
+}
+
 template <class F>
 void parallel(int T, F f) {
   if (T <= 1) { f(0); return; }
@@ -103,6 +116,41 @@ bool needs_python(const Mapped& f, int T) {
     }
   });
   return bad.load();
+}
+
+// Byte classes of 64 bytes at p (n <= 64 valid), SSE2 (x86-64 baseline): bit i
+// of nl = p[i] is '\n'; of odd = p[i] is outside "ACGTNacgtn\n"; of py = p[i]
+// is a byte Python's text mode decodes or translates (>= 0x80, '\r')
+struct ByteClasses {
+  uint64_t nl, odd, py;
+};
+inline ByteClasses classify64(const char* p, size_t n) {
+  alignas(16) char tail[64];
+  if (n < 64) {
+    memset(tail, '\n', sizeof(tail));  // padding: newlines, masked off below
+    memcpy(tail, p, n);
+    p = tail;
+  }
+  const __m128i df = _mm_set1_epi8((char)0xDF), nlv = _mm_set1_epi8('\n'), crv = _mm_set1_epi8('\r');
+  const __m128i A = _mm_set1_epi8('A'), C = _mm_set1_epi8('C'), G = _mm_set1_epi8('G'), T = _mm_set1_epi8('T'),
+                N = _mm_set1_epi8('N');
+  ByteClasses m{0, 0, 0};
+  for (int q = 0; q < 4; ++q) {
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * q));
+    const __m128i u = _mm_and_si128(v, df);  // upper() on ASCII letters; maps no other byte onto A C G T N
+    const __m128i nl = _mm_cmpeq_epi8(v, nlv);
+    const __m128i base = _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(u, A), _mm_cmpeq_epi8(u, C)),
+                                      _mm_or_si128(_mm_or_si128(_mm_cmpeq_epi8(u, G), _mm_cmpeq_epi8(u, T)),
+                                                   _mm_cmpeq_epi8(u, N)));
+    m.nl |= (uint64_t)(uint32_t)_mm_movemask_epi8(nl) << (16 * q);
+    m.odd |= (uint64_t)(~(uint32_t)_mm_movemask_epi8(_mm_or_si128(base, nl)) & 0xFFFFu) << (16 * q);
+    m.py |= (uint64_t)(uint32_t)(_mm_movemask_epi8(v) | _mm_movemask_epi8(_mm_cmpeq_epi8(v, crv))) << (16 * q);
+  }
+  if (n < 64) {
+    const uint64_t keep = ((uint64_t)1 << n) - 1;
+    m.nl &= keep; m.odd &= keep; m.py &= keep;
+  }
+  return m;
 }
 
 // [a, b) moved forward to line starts (a line = up to and including '\n'; a last
@@ -197,6 +245,54 @@ inline int64_t py_cut(int64_t L, int64_t k) {
   return k < 0 ? 0 : (k > L ? L : k);
 }
 
+// Read name -> record: open addressing, linear probing, built by all threads at
+// once.  A slot holds (hash high 32 bits << 32 | record index); empty = ~0.
+// Records of one name share the high bits, so keeping the MINIMUM slot value
+// (a CAS loop) keeps the name's first record in file order (:237-243) whatever
+// order the threads insert in.
+struct NameTable {
+  std::unique_ptr<std::atomic<uint64_t>[]> slot;
+  uint64_t mask = 0;
+  static uint64_t hash(sv name) { return (uint64_t)std::hash<sv>()(name); }
+  void init(int64_t n, int T) {
+    uint64_t cap = 1024;
+    while (cap < (uint64_t)n * 2) cap <<= 1;
+    slot.reset(new std::atomic<uint64_t>[cap]);
+    mask = cap - 1;
+    parallel(T, [&](int k) {
+      for (uint64_t i = cap * (uint64_t)k / (uint64_t)T; i < cap * (uint64_t)(k + 1) / (uint64_t)T; ++i)
+        slot[i].store(~(uint64_t)0, std::memory_order_relaxed);
+    });
+  }
+  // name_of(index) -> the name of a record already inserted
+  template <class NameOf>
+  void insert(uint32_t idx, sv name, uint64_t h, NameOf name_of) {
+    const uint64_t v = (h >> 32) << 32 | idx;
+    for (uint64_t p = h & mask;; p = (p + 1) & mask) {
+      uint64_t cur = slot[p].load(std::memory_order_relaxed);
+      for (;;) {
+        if (cur == ~(uint64_t)0) {
+          if (slot[p].compare_exchange_weak(cur, v, std::memory_order_relaxed)) return;
+          continue;  // cur reloaded
+        }
+        if ((cur >> 32) != (v >> 32) || name_of((uint32_t)cur) != name) break;  // another name: probe on
+        while (v < cur && !slot[p].compare_exchange_weak(cur, v, std::memory_order_relaxed)) {}
+        return;
+      }
+    }
+  }
+  // slot value of a name, ~0: absent
+  template <class NameOf>
+  uint64_t find(sv name, NameOf name_of) const {
+    const uint64_t h = hash(name);
+    for (uint64_t p = h & mask;; p = (p + 1) & mask) {
+      const uint64_t cur = slot[p].load(std::memory_order_relaxed);
+      if (cur == ~(uint64_t)0) return cur;
+      if ((cur >> 32) == (h >> 32) && name_of((uint32_t)cur) == name) return cur;
+    }
+  }
+};
+
 struct Flank {
   size_t pos = SIZE_MAX;  // file position of the record (duplicates: the last wins)
   std::string up, down;
@@ -209,16 +305,15 @@ struct Flank {
 struct Job {
   Mapped fr, fp;
   std::string ref;
-  std::vector<PafRec> keep;                              // first line per read name, file order
-  std::vector<std::unordered_map<sv, int64_t>> shard;    // name -> index in keep, sharded by hash
+  std::vector<PafRec> keep;  // first line per read name, file order
+  NameTable names;           // name -> index in keep
   std::vector<Flank> flanks;
   int64_t n_lines = 0;
   Fail fail;
   bool live = true;  // Steps 1-2 passed: take part in Step 3
   int64_t lookup(sv name) const {  // record of a read name, -1: not in this PAF
-    const auto& m = shard[(size_t)((uint32_t)std::hash<sv>()(name) % (uint32_t)shard.size())];
-    auto it = m.find(name);
-    return it == m.end() ? -1 : it->second;
+    const uint64_t v = names.find(name, [&](uint32_t i) { return keep[i].name; });
+    return v == ~(uint64_t)0 ? -1 : (int64_t)(uint32_t)v;
   }
 };
 
@@ -255,37 +350,54 @@ void job_ref_paf(Job& J, int T) {
   });
   for (auto& f : fails) J.fail.merge(f);
   if (J.fail.code != MPC_INGEST_OK) { J.live = false; return; }
+  phase("  paf lines");
   size_t total = 0;
   for (int k = 0; k < T; ++k) { J.n_lines += nlines[k]; total += recs[k].size(); }
-  // first line per name wins (:237-243).  Names are sharded by hash: thread s
-  // walks every record in file order and keeps the names of its shard in its
-  // own map, so the first occurrence is found without a serial pass over a
-  // million-entry map; the kept records are then compacted in file order.
+  if (total >= ((size_t)1 << 32) - 1) {
+    J.fail.set(MPC_INGEST_ERROR, 0, "more than 2^32 - 2 PAF lines (unsupported)");
+    J.live = false;
+    return;
+  }
+  // first line per name wins (:237-243): every thread inserts its own lines into
+  // one table (NameTable keeps the lowest line index per name), the winners are
+  // marked from the table and compacted in file order, and the table is then
+  // rewritten to hold indices into keep.
   std::vector<PafRec> all;
-  all.reserve(total);
-  for (int k = 0; k < T; ++k) all.insert(all.end(), recs[k].begin(), recs[k].end());
-  recs.clear();
-  const int64_t NA = (int64_t)all.size();
-  std::vector<uint32_t> hsh((size_t)NA);
+  all.resize(total);
+  std::vector<size_t> base((size_t)T + 1, 0);
+  for (int k = 0; k < T; ++k) base[(size_t)k + 1] = base[(size_t)k] + recs[(size_t)k].size();
+  const int64_t NA = (int64_t)total;
+  J.names.init(NA, T);
+  auto name_all = [&](uint32_t i) { return all[i].name; };
+  parallel(T, [&](int k) {
+    std::copy(recs[(size_t)k].begin(), recs[(size_t)k].end(), all.begin() + (ptrdiff_t)base[(size_t)k]);
+    std::vector<PafRec>().swap(recs[(size_t)k]);
+    for (size_t i = base[(size_t)k]; i < base[(size_t)k + 1]; ++i)
+      J.names.insert((uint32_t)i, all[i].name, NameTable::hash(all[i].name), name_all);
+  });
+  phase("  paf name table");
+  const uint64_t cap = J.names.mask + 1;
   std::vector<uint8_t> first((size_t)NA, 0);
   parallel(T, [&](int k) {
-    const std::hash<sv> h;
-    for (int64_t i = NA * k / T; i < NA * (k + 1) / T; ++i) hsh[(size_t)i] = (uint32_t)h(all[(size_t)i].name);
+    for (uint64_t p = cap * (uint64_t)k / (uint64_t)T; p < cap * (uint64_t)(k + 1) / (uint64_t)T; ++p) {
+      const uint64_t v = J.names.slot[p].load(std::memory_order_relaxed);
+      if (v != ~(uint64_t)0) first[(uint32_t)v] = 1;
+    }
   });
-  J.shard.resize((size_t)T);
+  phase("  paf first");
+  std::vector<uint32_t> kidx((size_t)NA);
+  uint32_t nk = 0;
+  for (int64_t i = 0; i < NA; ++i) { kidx[(size_t)i] = nk; nk += first[(size_t)i]; }
+  J.keep.resize(nk);
   parallel(T, [&](int k) {
-    auto& m = J.shard[(size_t)k];
-    m.reserve((size_t)(2 * NA / T + 16));
-    for (int64_t i = 0; i < NA; ++i)
-      if (hsh[(size_t)i] % (uint32_t)T == (uint32_t)k && m.emplace(all[(size_t)i].name, i).second) first[(size_t)i] = 1;
+    for (int64_t i = NA * k / T; i < NA * (k + 1) / T; ++i)
+      if (first[(size_t)i]) J.keep[kidx[(size_t)i]] = all[(size_t)i];
+    for (uint64_t p = cap * (uint64_t)k / (uint64_t)T; p < cap * (uint64_t)(k + 1) / (uint64_t)T; ++p) {
+      const uint64_t v = J.names.slot[p].load(std::memory_order_relaxed);
+      if (v != ~(uint64_t)0) J.names.slot[p].store((v >> 32) << 32 | kidx[(uint32_t)v], std::memory_order_relaxed);
+    }
   });
-  std::vector<int64_t> kidx((size_t)NA, -1);
-  J.keep.reserve((size_t)NA);
-  for (int64_t i = 0; i < NA; ++i)
-    if (first[(size_t)i]) { kidx[(size_t)i] = (int64_t)J.keep.size(); J.keep.push_back(all[(size_t)i]); }
-  parallel(T, [&](int k) {
-    for (auto& kv : J.shard[(size_t)k]) kv.second = kidx[(size_t)kv.second];
-  });
+  phase("  paf keep");
   J.flanks.resize(J.keep.size());
 }
 
@@ -294,11 +406,15 @@ void job_ref_paf(Job& J, int T) {
 // stay in the mapping as (start, rstripped length) spans and only the flank
 // bytes are copied out (a 10 kb read has ~80 flank bytes).
 // seq = "".join(line.rstrip().upper()) (:270), so seq[i] is upper() of the span
-// byte at position i.
-void jobs_fasta(std::vector<Job>& jobs, const Mapped& fa, int T) {
+// byte at position i.  Each byte is classified once (classify64): the line
+// ends, whether a line holds anything but bases (then, and only then, it is
+// rstripped and checked byte by byte) and the bytes that need Python's text
+// mode.  Returns true when the file holds such a byte (the caller falls back).
+bool jobs_fasta(std::vector<Job>& jobs, const Mapped& fa, int T) {
   const int nj = (int)jobs.size();
   std::mutex locks[64];
   std::vector<std::vector<Fail>> ffails((size_t)nj, std::vector<Fail>((size_t)T));
+  std::atomic<bool> py{false};
   auto rec_start = [&](size_t x) {  // first header line ('>' at a line start) at or after x
     size_t y = line_start_at_or_after(fa, x);
     while (y < fa.n && fa.p[y] != '>') {
@@ -315,6 +431,7 @@ void jobs_fasta(std::vector<Job>& jobs, const Mapped& fa, int T) {
     bool any = false;
     size_t cur_pos = 0;
     int valid = -1;  // every byte of the record in ACGTN after upper(): -1 not checked yet
+    bool rec_odd = false;  // a sequence byte of the record (after rstrip) is outside ACGTN after upper()
     char bad_c = '?';
     // copy seq[i0, i1) (upper-cased) to dst, forward
     auto copy_fwd = [&](int64_t i0, int64_t i1, char* dst) {
@@ -329,24 +446,18 @@ void jobs_fasta(std::vector<Job>& jobs, const Mapped& fa, int T) {
     // KeyError for any byte of the WHOLE sequence outside ACGTN (after upper();
     // for ASCII, (c & 0xDF) is upper() on letters and maps no other byte onto
     // A, C, G, T, N); the first offending byte in seq[::-1] order is reported
+    auto is_base = [](char ch) {
+      const unsigned u = (unsigned char)ch & 0xDFu;
+      return u == 'A' || u == 'C' || u == 'G' || u == 'T' || u == 'N';
+    };
     auto check_rc = [&]() {
       if (valid >= 0) return;
-      bool bad = false;
-      for (const sv& s : spans) {
-        unsigned ok = 1;
-        for (char ch : s) {
-          const unsigned u = (unsigned char)ch & 0xDFu;
-          ok &= (unsigned)((u == 'A') | (u == 'C') | (u == 'G') | (u == 'T') | (u == 'N'));
-        }
-        bad |= !ok;
-      }
+      const bool bad = rec_odd;
       valid = bad ? 0 : 1;
       if (bad)
         for (auto it = spans.rbegin(); it != spans.rend() && bad_c == '?'; ++it)
-          for (size_t i = it->size(); i-- > 0;) {
-            const unsigned u = (unsigned char)(*it)[i] & 0xDFu;
-            if (!(u == 'A' || u == 'C' || u == 'G' || u == 'T' || u == 'N')) { bad_c = upper((*it)[i]); break; }
-          }
+          for (size_t i = it->size(); i-- > 0;)
+            if (!is_base((*it)[i])) { bad_c = upper((*it)[i]); break; }
     };
     auto done = [&]() {  // :259-265 for the record just read, in every job whose PAF names it
       if (!any) return;
@@ -389,9 +500,8 @@ void jobs_fasta(std::vector<Job>& jobs, const Mapped& fa, int T) {
         }
       }
     };
-    for (size_t x = a; x < b;) {
-      const char* nl = static_cast<const char*>(memchr(fa.p + x, '\n', b - x));
-      const size_t e = nl ? (size_t)(nl - fa.p) : b;
+    // one line [x, e) without its '\n'; odd: it holds a byte outside "ACGTNacgtn"
+    auto line_at = [&](size_t x, size_t e, bool odd) {
       const sv line(fa.p + x, e - x);
       if (!line.empty() && line[0] == '>') {
         done();
@@ -403,22 +513,44 @@ void jobs_fasta(std::vector<Job>& jobs, const Mapped& fa, int T) {
         }
         cur_pos = x;
         valid = -1;
+        rec_odd = false;
         bad_c = '?';
         spans.clear();
         span_end.clear();
       } else if (any) {
-        const sv s = rstrip(line);  // :270
+        const sv s = odd ? rstrip(line) : line;  // :270 (a line of bases only has nothing to strip)
         if (!s.empty()) {
           spans.push_back(s);
           span_end.push_back((span_end.empty() ? 0 : span_end.back()) + (int64_t)s.size());
+          if (odd && !rec_odd)
+            for (char ch : s)
+              if (!is_base(ch)) { rec_odd = true; break; }
         }
       }
-      x = e + 1;
+    };
+    size_t ls = a;      // start of the current line
+    bool lodd = false;  // the current line holds a non-base byte so far
+    for (size_t blk = a, nb = 0; blk < b; blk += 64, ++nb) {
+      const ByteClasses m = classify64(fa.p + blk, std::min<size_t>(64, b - blk));
+      if (m.py || ((nb & 1023) == 0 && py.load(std::memory_order_relaxed))) { py = true; return; }
+      uint64_t nl = m.nl, odd = m.odd;
+      while (nl) {
+        const int i = __builtin_ctzll(nl);
+        line_at(ls, blk + (size_t)i, lodd || (odd & (((uint64_t)1 << i) - 1)) != 0);
+        ls = blk + (size_t)i + 1;
+        lodd = false;
+        nl &= nl - 1;
+        odd &= ~(((uint64_t)2 << i) - 1);  // bits <= i belong to finished lines
+      }
+      lodd |= odd != 0;
     }
+    if (ls < b) line_at(ls, b, lodd);  // a last line without '\n'
     done();
   });
+  if (py.load()) return true;
   for (int j = 0; j < nj; ++j)
     for (auto& f : ffails[(size_t)j]) jobs[(size_t)j].fail.merge(f);
+  return false;
 }
 
 // one job's result packed in PAF first-occurrence order (:292)
@@ -487,6 +619,7 @@ void mpc_ingest_free(mpc_ingest_out* o) {
 int mpc_ingest_multi(int n_jobs, const char* const* ref_paths, const char* const* paf_paths, const char* reads_path,
                      int n_threads, mpc_ingest_out* outs) {
   if (n_jobs <= 0) return MPC_INGEST_OK;
+  phase(nullptr);
   for (int j = 0; j < n_jobs; ++j) memset(&outs[j], 0, sizeof(outs[j]));
   auto finish = [&](mpc_ingest_out* out, int code, const std::string& msg) {
     out->status = code;
@@ -509,27 +642,34 @@ int mpc_ingest_multi(int n_jobs, const char* const* ref_paths, const char* const
   }
   Mapped fa;
   const bool fa_ok = fa.open(reads_path);
-  if (fa_ok && needs_python(fa, T))
-    return finish_all(MPC_INGEST_FALLBACK, "non-ASCII byte or carriage return: Python text-mode semantics");
+  phase("open");
   for (auto& J : jobs) {
     if (!J.live) continue;
-    if (needs_python(J.fr, T) || needs_python(J.fp, T)) {
+    const bool py = needs_python(J.fr, T) || needs_python(J.fp, T);
+    phase("  ascii ref+paf");
+    if (py) {
       J.fail.set(MPC_INGEST_FALLBACK, 0, "non-ASCII byte or carriage return: Python text-mode semantics");
       J.live = false;
       continue;
     }
     job_ref_paf(J, T);
+    phase("ref+paf");
     if (J.live && !fa_ok) {
       J.fail.set(MPC_INGEST_ERROR, 0, std::string("cannot open ") + reads_path);
       J.live = false;
     }
   }
-  if (fa_ok) jobs_fasta(jobs, fa, T);
+  // the reads file is checked for Python text-mode bytes in the same pass; such
+  // a byte sends every job to Python, whatever else failed
+  if (fa_ok && jobs_fasta(jobs, fa, T))
+    return finish_all(MPC_INGEST_FALLBACK, "non-ASCII byte or carriage return: Python text-mode semantics");
+  phase("reads fasta");
   for (int j = 0; j < n_jobs; ++j) {
     Job& J = jobs[(size_t)j];
     if (J.fail.code == MPC_INGEST_OK) job_pack(J, T, &outs[j]);
     finish(&outs[j], J.fail.code, J.fail.msg);
   }
+  phase("pack");
   return outs[0].status;
 }
 

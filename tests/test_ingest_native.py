@@ -173,3 +173,55 @@ def test_multi_job_shared_reads(ing, tmp_path):
     assert isinstance(r[0], dict) and isinstance(r[1], ing.IngestError)
     with pytest.raises(ing.IngestError):
         ing.pack_samples(jobs + [(str(tmp_path / "r1.fa"), str(tmp_path / "p3.paf"), str(reads))])
+
+
+def _fuzz_files(rng, tmp_path, interior, trailing):
+    """Random FASTA/PAF text: line lengths around the 64-byte blocks of the native
+    scan, lower case, trailing whitespace, rare non-base bytes, blank lines,
+    duplicate names in both files, records no PAF line names."""
+    names = [f"r{i}" for i in range(60)]
+    recs = []
+    for r in range(90):  # every name once (no KeyError for a missing read), then duplicates
+        nm = names[r] if r < len(names) else names[int(rng.integers(len(names)))]
+        lines = []
+        for _ in range(int(rng.integers(0, 5))):
+            L = int(rng.choice([0, 1, 63, 64, 65, 127, 128, 129, int(rng.integers(0, 300))]))
+            s = "".join(rng.choice(list("ACGTNacgtn"), size=L))
+            if L and rng.random() < interior:
+                k = int(rng.integers(L))
+                s = s[:k] + str(rng.choice(list("X .*\t"))) + s[k + 1:]
+            if rng.random() < trailing:
+                s += str(rng.choice([" ", "\t", "  \t", "\x0b"]))
+            lines.append(s)
+        recs.append(">" + nm + ("\n" + "\n".join(lines) if lines else "") + "\n")
+    rng.shuffle(recs)
+    reads = "".join(recs)
+    paf = ""
+    for _ in range(80):
+        nm = names[int(rng.integers(len(names)))]
+        qlen = int(rng.integers(1, 400))
+        qs, qe = sorted(int(x) for x in rng.integers(-5, qlen + 5, size=2))
+        paf += paf_line(nm, qlen, qs, qe, "-" if rng.random() < 0.5 else "+", int(rng.integers(0, 5)), ":3")
+    return _files(tmp_path, ">r\nACGTACGTACGT\n", paf, reads)
+
+
+@pytest.mark.parametrize("seed", range(12))
+def test_fuzz_block_scan_and_name_table(ing, seed, tmp_path):
+    """The byte-class scan (64-byte blocks, fast path for lines of bases only) and
+    the shared name table give the Python result on random text, for any thread
+    count.  Non-base bytes inside lines (a minus-strand KeyError) in a third of
+    the seeds; trailing whitespace (stripped, no error) in two thirds."""
+    rng = np.random.default_rng(seed)
+    interior = 0.08 if seed % 3 == 1 else 0.0
+    paths = _fuzz_files(rng, tmp_path, interior, 0.0 if seed % 3 == 2 else 0.15)
+    nat = _same(ing, *paths)
+    if not interior:
+        assert nat is not None and len(nat["tstart"]) > 20
+    for n_threads in (1, 2, 5, 16):
+        try:
+            c = ing.pack_sample_native(*paths, n_threads=n_threads)
+        except ing.IngestError:
+            assert nat is None
+            continue
+        for k in KEYS:
+            assert np.array_equal(np.asarray(c[k]), np.asarray(nat[k])), (n_threads, k)

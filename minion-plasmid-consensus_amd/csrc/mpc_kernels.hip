@@ -275,6 +275,11 @@ template <int WIN> constexpr int tok_cap() { return WIN <= 1024 ? WIN : 1024; }
 #define MPC_PARSE_DMA 1
 #endif
 template <int WIN> constexpr bool parse_dma() { return MPC_PARSE_DMA && WIN >= 1024; }
+// K_parse tally modes (bit TM) whose rounds try the fast decode first
+#ifndef MPC_FAST_DECODE_MODES
+#define MPC_FAST_DECODE_MODES 0x18
+#endif
+template <int TM> constexpr bool fast_decode() { return (MPC_FAST_DECODE_MODES >> TM) & 1; }
 template <int WIN> constexpr int stage_bufs() { return parse_dma<WIN>() ? 2 : 1; }
 
 template <int WIN>
@@ -1049,8 +1054,8 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const uint32_t* b32 = reinterpret_cast<const uint32_t*>(W.stage[sb]);
       int adv0, adv, kind, olen_e;
       uint32_t pay, err = 0u;
-      bool fast;
-      {
+      bool fast = false;
+      if constexpr (fast_decode<TM>()) {
         const uint32_t sh = (uint32_t)(sx & 3);
         uint32_t m0 = b32[sx >> 2], m1 = b32[(sx >> 2) + 1];  // bytes sx .. sx + 4 (sh + 4 <= 7)
         const int pa = (s0 + 1) >> 2;
@@ -1095,7 +1100,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         pay = (ms & ((codes >> shl) & 3u)) | (~ms & pk);
         olen_e = ol4;
       }
-      if (ballot(!fast)) {  // general decode of the whole round
+      if (!fast_decode<TM>() || ballot(!fast)) {  // general decode of the whole round
         const int a4 = sx >> 2;
         const uint32_t sh = (uint32_t)(sx & 3);
         const uint32_t d0 = b32[a4], d1 = b32[a4 + 1], d2 = b32[a4 + 2];
@@ -1474,9 +1479,69 @@ __device__ __forceinline__ void rsort_pass(const uint32_t* sk, const int32_t* sv
   __syncthreads();
 }
 
+// Register path of K_rsort (more entries than the LDS path holds, up to
+// kRS * kRegE): an entry is ONE word, gap << sb | its index in read order (sb
+// bits), so the stable gap passes keep read order and need one LDS buffer: the
+// entries of a pass's source order sit in VGPRs (wave w: positions s0 + 64 u +
+// lane), the scatter writes the new order into LDS, and every wave reloads its
+// positions from there.  The values (global reads) wait in HBM at their index.
+constexpr int kRegE = 32;
+__device__ __forceinline__ void rsort_reg_pass(uint32_t (&e)[kRegE], int64_t s0, int64_t s1, int sh, uint32_t* buf,
+                                               int32_t (*wc)[256], int32_t* hb, bool reload) {
+  constexpr int NW = kRS / 64;
+  const int tid = threadIdx.x, l = lane(), w = tid >> 6;
+  const uint64_t lt = (1ull << l) - 1ull;
+  for (int k = l; k < 256; k += 64) wc[w][k] = 0;
+#pragma unroll
+  for (int u = 0; u < kRegE; ++u)
+    if (s0 + 64 * u + l < s1) atomicAdd(&wc[w][(e[u] >> sh) & 255u], 1);
+  __syncthreads();
+  if (tid < 256) {
+    int t = 0;
+    for (int k = 0; k < NW; ++k) t += wc[k][tid];
+    hb[tid] = t;
+  }
+  __syncthreads();
+  if (tid < 64) {
+    const int x0 = hb[4 * tid], x1 = hb[4 * tid + 1], x2 = hb[4 * tid + 2], x3 = hb[4 * tid + 3];
+    const int t4 = x0 + x1 + x2 + x3;
+    const int ex = wave_scan_i32(t4) - t4;
+    hb[4 * tid] = ex; hb[4 * tid + 1] = ex + x0; hb[4 * tid + 2] = ex + x0 + x1; hb[4 * tid + 3] = ex + x0 + x1 + x2;
+  }
+  __syncthreads();
+  if (tid < 256) {
+    int run = hb[tid];
+    for (int k = 0; k < NW; ++k) { const int c = wc[k][tid]; wc[k][tid] = run; run += c; }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int u = 0; u < kRegE; ++u) {
+    const bool v = s0 + 64 * u + l < s1;
+    if (ballot(v) == 0) break;  // (wave-uniform) the wave's positions are used up
+    const uint32_t dg = (e[u] >> sh) & 255u;
+    uint64_t m = ballot(v);
+#pragma unroll
+    for (int bit = 0; bit < 8; ++bit) {
+      const uint64_t bb = ballot(((dg >> bit) & 1u) != 0);
+      m &= ((dg >> bit) & 1u) ? bb : ~bb;
+    }
+    const int rank = __popcll(m & lt);
+    const int base = v ? wc[w][dg] : 0;
+    if (v) buf[base + rank] = e[u];
+    if (v && rank == 0) wc[w][dg] = base + __popcll(m);
+  }
+  __syncthreads();
+  if (reload) {
+#pragma unroll
+    for (int u = 0; u < kRegE; ++u)
+      if (s0 + 64 * u + l < s1) e[u] = buf[s0 + 64 * u + l];
+  }
+}
+
 __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t end_bit) {
-  __shared__ uint32_t lk[2][kSortLds];
-  __shared__ int32_t lv[2][kSortLds];
+  __shared__ uint32_t pool[4 * kSortLds];  // LDS path: keys and values, two buffers each; register path: one buffer
+  uint32_t (*lk)[kSortLds] = reinterpret_cast<uint32_t (*)[kSortLds]>(pool);
+  int32_t (*lv)[kSortLds] = reinterpret_cast<int32_t (*)[kSortLds]>(pool + 2 * kSortLds);
   __shared__ int32_t wc[kRS / 64][256];
   __shared__ int32_t hb[256];
   __shared__ int32_t s_w[kRS / 64];
@@ -1508,6 +1573,52 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
   if (M == 0) return;
   const int passes = (end_bit + 7) / 8;
   const bool in_lds = M <= kSortLds;
+  const int sb = 32 - __clz((uint32_t)(M - 1) | 1u);  // bits of an entry index (register path)
+  if (!in_lds && M <= (int64_t)kRS * kRegE && end_bit + sb <= 32) {
+    // ---- register path: gather gap << sb | index into LDS (values to HBM), one source block per thread ----
+    for (int b = tid; b < nblocks; b += kRS) {
+      const int c = d.bcnt[b];
+      const int o = d.bpre[b];
+      const uint32_t* ks = d.keys_in + (int64_t)b * kRS;
+      const int32_t* vs = d.vals_in + (int64_t)b * kRS;
+      for (int j0 = 0; j0 < c; j0 += 8) {
+        uint32_t kk[8];
+        int32_t vv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int j = j0 + u < c ? j0 + u : c - 1;
+          kk[u] = ks[j];
+          vv[u] = vs[j];
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+          if (j0 + u < c) { pool[o + j0 + u] = kk[u] << sb | (uint32_t)(o + j0 + u); d.vals_tmp[o + j0 + u] = vv[u]; }
+      }
+    }
+    __syncthreads();
+    constexpr int NW = kRS / 64;
+    const int64_t s0 = M * w / NW, s1 = M * (w + 1) / NW;  // <= 64 kRegE positions per wave
+    uint32_t e[kRegE];
+#pragma unroll
+    for (int u = 0; u < kRegE; ++u) e[u] = s0 + 64 * u + l < s1 ? pool[s0 + 64 * u + l] : 0u;
+    __syncthreads();  // every wave holds its entries before the first scatter
+    for (int p = 0; p < passes; ++p) rsort_reg_pass(e, s0, s1, sb + 8 * p, pool, wc, hb, p + 1 < passes);
+    const uint32_t im = (1u << sb) - 1u;  // (sb <= 15 here)
+    for (int64_t i0 = 0; i0 < M; i0 += 4 * kRS) {
+      uint32_t x[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { const int64_t i = i0 + tid + u * kRS; x[u] = i < M ? pool[i] : 0u; }
+      int32_t vv[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) { const int64_t i = i0 + tid + u * kRS; vv[u] = i < M ? d.vals_tmp[x[u] & im] : 0; }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const int64_t i = i0 + tid + u * kRS;
+        if (i < M) { d.keys_out[i] = x[u] >> sb; d.vals_out[i] = vv[u]; }
+      }
+    }
+    return;
+  }
   uint32_t* kb[2];
   int32_t* vb[2];
   if (in_lds) { kb[0] = lk[0]; kb[1] = lk[1]; vb[0] = lv[0]; vb[1] = lv[1]; }

@@ -252,6 +252,11 @@ class Batch:
         self.parse_cus = int(parse_cus)
 
         def cat_bytes(key, offkey):
+            if S == 1:  # one sample: its buffer as is (no copy of a GB of cs)
+                b = np.asarray(samples[0][key], dtype=np.uint8)
+                o = np.asarray(samples[0][offkey], dtype=np.int64)
+                if len(o) and o[0] == 0:
+                    return b[:o[-1]], o
             bufs, offs, base = [], [], 0
             for s in samples:
                 b = np.asarray(s[key], dtype=np.uint8)

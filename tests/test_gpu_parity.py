@@ -327,3 +327,22 @@ def test_reference_past_coordinate_limit(pkg):
             "down_off": np.zeros(2, np.int64)}
     with pytest.raises(pkg.engine.MpcError):
         pkg.engine.Plan(pkg.engine.Batch([long]))
+
+
+@pytest.mark.parametrize("spec,lo,hi", [
+    # K_rsort's three paths by the count M of mixed RIGHT events (status word
+    # MPC_ST_MIXED): LDS (M <= 8192), register (<= 32768 entries of one word),
+    # HBM ping-pong beyond
+    (dict(n=400, n_reads=4000, profile="indel", seed=4, frac_partial=0.5), 1, 8192),
+    (dict(n=1000, n_reads=30000, profile="indel", seed=5, frac_partial=0.5), 8193, 32768),
+    (dict(n=3000, n_reads=60000, profile="indel", seed=6, frac_partial=0.6), 32769, 10 ** 9),
+], ids=["lds", "registers", "hbm"])
+def test_mixed_right_sort_paths(pkg, spec, lo, hi):
+    syn = pkg.synth.Synth(antisense=False, **spec)
+    samples = [syn.sample(0)]
+    runner = pkg.engine.Runner(samples)
+    runner.step(-1.0, 1.0)
+    runner.check()
+    m = int(runner.plan.status()[pkg.engine.MPC_ST_MIXED])
+    assert lo <= m <= hi, m
+    _cmp(runner.fetch()[0], _oracle(samples[0], -1.0, 1.0), ("rsort", m))

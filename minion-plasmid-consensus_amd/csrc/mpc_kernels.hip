@@ -268,22 +268,34 @@ constexpr int kMaxCh = MPC_PARSE_CHUNKS;  // read chunks per parse workgroup, ta
 // would hold more (LDS budget), smaller windows never hold more than WIN
 template <int WIN> constexpr int tok_cap() { return WIN <= 1024 ? WIN : 1024; }
 
-// K_parse stages a window's cs bytes by LDS-DMA (global_load_lds_dwordx4,
+// K_parse may stage a window's cs bytes by LDS-DMA (global_load_lds_dwordx4,
 // no VGPRs) into the other of two per-wave stage buffers while the current
-// window's rounds run (windows of 1-2 KiB; 512-byte windows load into VGPRs)
+// window's rounds run.  Off: measured slower at every config (C1 +15 %, C5
+// +14 %, C2-C4 +1 %; profiles/r04_experiments/kparse_variants.txt) -- the
+// consumer's vmcnt(0) also waits for every event store the rounds issued.
 #ifndef MPC_PARSE_DMA
-#define MPC_PARSE_DMA 1
+#define MPC_PARSE_DMA 0
 #endif
 template <int WIN> constexpr bool parse_dma() { return MPC_PARSE_DMA && WIN >= 1024; }
 // K_parse tally modes (bit TM) whose rounds try the fast decode first
+// (measured: C4 -4.5 %, C5 -2 %, C3 +0.6 %, C2 (mode 1) +8 %)
 #ifndef MPC_FAST_DECODE_MODES
 #define MPC_FAST_DECODE_MODES 0x18
 #endif
 template <int TM> constexpr bool fast_decode() { return (MPC_FAST_DECODE_MODES >> TM) & 1; }
+// ... and tally modes whose rounds find a unit's read base by an LDS round trip
+// (slot base written by the read's start lane, read back by every lane) instead
+// of a scalar pass over the round's read starts: short reads (C1 / C2) start
+// several reads per round
+#ifndef MPC_LDS_BASE_MODES
+#define MPC_LDS_BASE_MODES 0x07
+#endif
+template <int TM> constexpr bool lds_base() { return (MPC_LDS_BASE_MODES >> TM) & 1; }
 template <int WIN> constexpr int stage_bufs() { return parse_dma<WIN>() ? 2 : 1; }
 
 template <int WIN>
 struct alignas(16) WaveLds {            // per-wave LDS of K_parse
+  int32_t s_val[kSlots];                // read base (lds_base modes): i = s_val + window prefix of advances
   int32_t s_ts[kSlots];                 // tstart (clamped; -1: negative)
   int32_t s_read[kSlots];               // local read index
   int32_t s_iend[kSlots];               // i_end | bit 30: read has a downstream flank
@@ -1178,10 +1190,17 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       // scalar pass over the start lanes (about one per round: reads hold tens
       // to hundreds of units) instead of an LDS write, fence and read back
       int bv = cb;
-      for (uint64_t m = brs; m; m &= m - 1) {
-        const int j = __ffsll((unsigned long long)m) - 1;
-        cb = __builtin_amdgcn_readlane(q_ts, j) - (G + __builtin_amdgcn_readlane(aex, j));
-        bv = l >= j ? cb : bv;
+      if constexpr (lds_base<TM>()) {
+        if (is_rs) W.s_val[q] = q_ts - (G + aex);
+        wave_sync_lds();
+        const int sv = W.s_val[q];
+        bv = q == 0 ? cb : sv;  // slot 0: the read open since an earlier window
+      } else {
+        for (uint64_t m = brs; m; m &= m - 1) {
+          const int j = __ffsll((unsigned long long)m) - 1;
+          cb = __builtin_amdgcn_readlane(q_ts, j) - (G + __builtin_amdgcn_readlane(aex, j));
+          bv = l >= j ? cb : bv;
+        }
       }
       const int iu = bv + G + aex;  // coordinate at the unit start
       const int i = iu + adv0;                // ... and at its main token
@@ -1246,6 +1265,8 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     // ---- reads that ended in this window: i_end; carry the open one ----
     if (l <= nst && (l > 0 || carry) && W.s_end[l] <= C) a.i_end[W.s_read[l]] = W.s_iend[l] & ~(1 << 30);
     const bool cont = (nst > 0 || carry) && W.s_end[nst] > C;
+    if constexpr (lds_base<TM>())
+      if (nst > 0) cb = uniform_i32(W.s_val[nst]);  // the base of the window's last read start
     if (cont) {
       const int64_t v = (int64_t)cb + G;
       c_base = (int32_t)(v > kICap ? kICap : v);

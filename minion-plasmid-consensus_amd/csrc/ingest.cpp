@@ -50,6 +50,9 @@ struct Mapped {
   int fd = -1;
   Mapped() = default;
   Mapped(const Mapped&) = delete;
+  Mapped(Mapped&& o) noexcept : p(o.p), n(o.n), m(o.m), fd(o.fd) {
+    o.p = ""; o.n = 0; o.m = nullptr; o.fd = -1;
+  }
   ~Mapped() {
     if (m && m != MAP_FAILED) munmap(m, n);
     if (fd >= 0) close(fd);
@@ -149,6 +152,29 @@ inline ByteClasses classify64(const char* p, size_t n) {
   if (n < 64) {
     const uint64_t keep = ((uint64_t)1 << n) - 1;
     m.nl &= keep; m.odd &= keep; m.py &= keep;
+  }
+  return m;
+}
+
+// PAF byte classes of 64 bytes at p (n <= 64 valid): bit i of nl / tab = p[i]
+// is '\n' / '\t'; of py as in classify64
+struct PafClasses {
+  uint64_t nl, tab, py;
+};
+inline PafClasses classify_paf64(const char* p, size_t n) {
+  alignas(16) char tail[64];
+  if (n < 64) {
+    memset(tail, ' ', sizeof(tail));
+    memcpy(tail, p, n);
+    p = tail;
+  }
+  const __m128i nlv = _mm_set1_epi8('\n'), tbv = _mm_set1_epi8('\t'), crv = _mm_set1_epi8('\r');
+  PafClasses m{0, 0, 0};
+  for (int q = 0; q < 4; ++q) {
+    const __m128i v = _mm_loadu_si128(reinterpret_cast<const __m128i*>(p + 16 * q));
+    m.nl |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(v, nlv)) << (16 * q);
+    m.tab |= (uint64_t)(uint32_t)_mm_movemask_epi8(_mm_cmpeq_epi8(v, tbv)) << (16 * q);
+    m.py |= (uint64_t)(uint32_t)(_mm_movemask_epi8(v) | _mm_movemask_epi8(_mm_cmpeq_epi8(v, crv))) << (16 * q);
   }
   return m;
 }
@@ -334,20 +360,84 @@ void job_ref_paf(Job& J, int T) {
   std::vector<std::vector<PafRec>> recs(T);
   std::vector<Fail> fails(T);
   std::vector<int64_t> nlines(T, 0);
+  // One classified pass (classify_paf64): line ends, the first 8 tab positions
+  // and the first field starting "cs:" of every line, and the Python text-mode
+  // bytes (the job falls back).  A line of >= 8 fields with a cs tag and plain
+  // integers is read from those positions; any other line goes through
+  // parse_paf_line for the reference's exact error.
+  std::atomic<bool> py{false};
   parallel(T, [&](int k) {
     const size_t a = line_start_at_or_after(fp, fp.n * k / T), b = line_start_at_or_after(fp, fp.n * (k + 1) / T);
-    for (size_t x = a; x < b;) {
-      const char* nl = static_cast<const char*>(memchr(fp.p + x, '\n', b - x));
-      const size_t e = nl ? (size_t)(nl - fp.p) : b;
+    size_t tabs[8];
+    int ntab = 0;
+    size_t cs0 = SIZE_MAX, cs1 = SIZE_MAX;  // the cs field's value [cs0, cs1) (cs1: the next tab)
+    auto slow = [&](size_t x, size_t e) {
       PafRec r;
       std::string err;
-      ++nlines[k];
       const int rc = parse_paf_line(sv(fp.p + x, e - x), &r, &err);
       if (rc == MPC_INGEST_OK) recs[k].push_back(r);
       else fails[k].set(rc, x, rc == MPC_INGEST_ERROR ? "PAF line: " + err : std::string("PAF integer field for Python"));
-      x = e + 1;
+    };
+    auto line_at = [&](size_t x, size_t e) {  // [x, e): the line without '\n'
+      ++nlines[k];
+      size_t re = e;  // rstrip()
+      while (re > x && py_space((unsigned char)fp.p[re - 1])) --re;
+      int nt = ntab < 8 ? ntab : 8;  // (fields 0-7 need the first 8 tabs only)
+      while (nt > 0 && tabs[nt - 1] >= re) --nt;  // tabs in the stripped tail split nothing
+      if (nt < 7 || cs0 == SIZE_MAX || cs0 > re) { slow(x, e); return; }  // < 8 fields or no cs: exact error
+      auto fld = [&](int i) {
+        const size_t f0 = i == 0 ? x : tabs[i - 1] + 1;
+        const size_t f1 = i < nt ? tabs[i] : re;
+        return sv(fp.p + f0, f1 - f0);
+      };
+      PafRec r;
+      int64_t qlen = 0, qs = 0, qe = 0, ts = 0;
+      if (plain_int(fld(1), &qlen) | plain_int(fld(2), &qs) | plain_int(fld(3), &qe) | plain_int(fld(7), &ts)) {
+        slow(x, e);
+        return;
+      }
+      r.name = fld(0);
+      r.minus = fld(4) == "-";
+      if (r.minus) { const int64_t u = qlen - qe, v = qlen - qs; qs = u; qe = v; }  // :226-228
+      const size_t ce = cs1 < re ? cs1 : re;
+      r.cs = sv(fp.p + cs0, ce - cs0);
+      r.qs = qs; r.qe = qe; r.ts = ts;
+      recs[k].push_back(r);
+    };
+    auto field_start = [&](size_t f) {  // a field starts at f: the first "cs:" one is the tag
+      if (cs0 == SIZE_MAX && f + 3 <= fp.n && fp.p[f] == 'c' && fp.p[f + 1] == 's' && fp.p[f + 2] == ':') cs0 = f + 3;
+    };
+    size_t ls = a;
+    if (a < b) field_start(a);
+    for (size_t blk = a, nb = 0; blk < b; blk += 64, ++nb) {
+      const PafClasses m = classify_paf64(fp.p + blk, std::min<size_t>(64, b - blk));
+      if (m.py || ((nb & 1023) == 0 && py.load(std::memory_order_relaxed))) { py = true; return; }
+      uint64_t ev = m.nl | m.tab;
+      while (ev) {
+        const int i = __builtin_ctzll(ev);
+        ev &= ev - 1;
+        const size_t pos = blk + (size_t)i;
+        if ((m.tab >> i) & 1u) {
+          if (ntab < 8) tabs[ntab] = pos;
+          ++ntab;
+          if (cs0 != SIZE_MAX && cs1 == SIZE_MAX && pos >= cs0) cs1 = pos;
+          if (pos + 1 < b) field_start(pos + 1);
+        } else {
+          line_at(ls, pos);
+          ls = pos + 1;
+          ntab = 0;
+          cs0 = cs1 = SIZE_MAX;
+          if (ls < b) field_start(ls);
+        }
+      }
     }
+    if (ls < b) line_at(ls, b);  // a last line without '\n'
   });
+  if (py.load()) {
+    J.fail.set(MPC_INGEST_FALLBACK, 0, "non-ASCII byte or carriage return: Python text-mode semantics");
+    J.live = false;
+    return;
+  }
   for (auto& f : fails) J.fail.merge(f);
   if (J.fail.code != MPC_INGEST_OK) { J.live = false; return; }
   phase("  paf lines");
@@ -553,6 +643,40 @@ bool jobs_fasta(std::vector<Job>& jobs, const Mapped& fa, int T) {
   return false;
 }
 
+// Output buffers.  Large ones (a GB of cs at C3) are anonymous mappings on
+// transparent huge pages: written once right after allocation, 4 KiB pages
+// cost a fault each (the fresh-page writes took ~2x the copy) and a slow
+// unmap.  A 64-byte header before the data records how to release it.
+constexpr size_t kHuge = (size_t)2 << 20;
+struct OutHeader {
+  uint64_t magic;
+  void* base;
+  size_t len;
+};
+constexpr uint64_t kMagicMalloc = 0x6d70636d616c6c63ull, kMagicMap = 0x6d70636d6d617070ull;
+void* out_alloc(size_t n) {
+  if (n >= 2 * kHuge) {
+    const size_t len = n + 64 + kHuge;
+    void* m = mmap(nullptr, len, PROT_READ | PROT_WRITE, MAP_PRIVATE | MAP_ANONYMOUS, -1, 0);
+    if (m != MAP_FAILED) {
+      uint8_t* a = reinterpret_cast<uint8_t*>(((uintptr_t)m + kHuge - 1) & ~(uintptr_t)(kHuge - 1));
+      madvise(a, len - (size_t)(a - (uint8_t*)m), MADV_HUGEPAGE);
+      *reinterpret_cast<OutHeader*>(a) = OutHeader{kMagicMap, m, len};
+      return a + 64;
+    }
+  }
+  uint8_t* a = static_cast<uint8_t*>(malloc(n + 64));
+  if (!a) return nullptr;
+  *reinterpret_cast<OutHeader*>(a) = OutHeader{kMagicMalloc, a, n + 64};
+  return a + 64;
+}
+void out_free(void* p) {
+  if (!p) return;
+  const OutHeader h = *reinterpret_cast<const OutHeader*>(static_cast<uint8_t*>(p) - 64);
+  if (h.magic == kMagicMap) munmap(h.base, h.len);
+  else free(h.base);
+}
+
 // one job's result packed in PAF first-occurrence order (:292)
 void job_pack(Job& J, int T, mpc_ingest_out* out) {
   const int64_t N = (int64_t)J.keep.size();
@@ -571,7 +695,7 @@ void job_pack(Job& J, int T, mpc_ingest_out* out) {
     }
     ncs += r.cs.size(); nup += f.up.size(); ndn += f.down.size();
   }
-  auto alloc = [](size_t n) { return malloc(n ? n : 1); };
+  auto alloc = [](size_t n) { return out_alloc(n); };
   out->ref = (uint8_t*)alloc(J.ref.size());
   memcpy(out->ref, J.ref.data(), J.ref.size());
   out->ref_len = (int64_t)J.ref.size();
@@ -602,6 +726,22 @@ void job_pack(Job& J, int T, mpc_ingest_out* out) {
   out->n_alignments = J.n_lines;
 }
 
+// The mappings (GBs of page-cache pages: unmapping 10 GB costs ~0.2 s) and the
+// name tables are released by a detached thread, off the caller's clock: the
+// results are copies, nothing points into them any more.
+void release_async(std::vector<Job>&& jobs, Mapped&& fa) {
+  struct Held {
+    std::vector<Job> jobs;
+    Mapped fa;
+  };
+  Held* h = new Held{std::move(jobs), std::move(fa)};
+  try {
+    std::thread([h] { delete h; }).detach();
+  } catch (...) {  // no thread: release here
+    delete h;
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -610,8 +750,8 @@ int mpc_ingest_version(void) { return 3; }  // 3: + mpc_ingest_multi; 2: + mpc_w
 
 void mpc_ingest_free(mpc_ingest_out* o) {
   if (!o) return;
-  free(o->ref); free(o->cs); free(o->cs_off); free(o->tstart); free(o->up); free(o->up_off);
-  free(o->down); free(o->down_off); free(o->aligned);
+  out_free(o->ref); out_free(o->cs); out_free(o->cs_off); out_free(o->tstart); out_free(o->up); out_free(o->up_off);
+  out_free(o->down); out_free(o->down_off); out_free(o->aligned);
   o->ref = o->cs = o->up = o->down = nullptr;
   o->cs_off = o->tstart = o->up_off = o->down_off = o->aligned = nullptr;
 }
@@ -645,8 +785,8 @@ int mpc_ingest_multi(int n_jobs, const char* const* ref_paths, const char* const
   phase("open");
   for (auto& J : jobs) {
     if (!J.live) continue;
-    const bool py = needs_python(J.fr, T) || needs_python(J.fp, T);
-    phase("  ascii ref+paf");
+    const bool py = needs_python(J.fr, T);  // (the PAF is checked in its parse pass)
+    phase("  ascii ref");
     if (py) {
       J.fail.set(MPC_INGEST_FALLBACK, 0, "non-ASCII byte or carriage return: Python text-mode semantics");
       J.live = false;
@@ -670,6 +810,8 @@ int mpc_ingest_multi(int n_jobs, const char* const* ref_paths, const char* const
     finish(&outs[j], J.fail.code, J.fail.msg);
   }
   phase("pack");
+  release_async(std::move(jobs), std::move(fa));
+  phase("release");
   return outs[0].status;
 }
 

@@ -291,11 +291,12 @@ template <int TM> constexpr bool fast_decode() { return (MPC_FAST_DECODE_MODES >
 #define MPC_LDS_BASE_MODES 0x07
 #endif
 template <int TM> constexpr bool lds_base() { return (MPC_LDS_BASE_MODES >> TM) & 1; }
+__host__ __device__ constexpr bool lds_base_rt(int tm) { return (MPC_LDS_BASE_MODES >> tm) & 1; }
 template <int WIN> constexpr int stage_bufs() { return parse_dma<WIN>() ? 2 : 1; }
 
-template <int WIN>
+template <int WIN, bool SV>              // SV: the read-base slots (lds_base modes)
 struct alignas(16) WaveLds {            // per-wave LDS of K_parse
-  int32_t s_val[kSlots];                // read base (lds_base modes): i = s_val + window prefix of advances
+  int32_t s_val[SV ? kSlots : 0];       // read base: i = s_val + window prefix of advances
   int32_t s_ts[kSlots];                 // tstart (clamped; -1: negative)
   int32_t s_read[kSlots];               // local read index
   int32_t s_iend[kSlots];               // i_end | bit 30: read has a downstream flank
@@ -341,11 +342,12 @@ template <int WIN>
 // (the depth difference as one biased 16-bit half), 3 = depth differences in
 // LDS (2 B per position), substitutions global: references up to ~40 kb
 __host__ __device__ inline int parse_lds_bytes(int n_max, int tm, int nbmax, int nw) {
-  if (tm == 4) return nw * (int)sizeof(WaveLds<WIN>) + parse_misc_bytes();  // per-gap state in HBM
+  const int wl = lds_base_rt(tm) ? (int)sizeof(WaveLds<WIN, true>) : (int)sizeof(WaveLds<WIN, false>);
+  if (tm == 4) return nw * wl + parse_misc_bytes();  // per-gap state in HBM
   const int tallies = tm == 0 ? 0 : tm == 1 ? 12 * (n_max + 1) : tm == 2 ? 8 * (n_max + 1) + 4 * ((n_max + 2) / 2)
                                                                  : 4 * ((n_max + 2) / 2);
   const int buckets = 16 * nbmax + 4;  // epilogue: counts, cursors, chunk counts, chunk offsets
-  return nw * (int)sizeof(WaveLds<WIN>) + parse_misc_bytes() + 4 * parse_hl_words(n_max) + 4 * nbmax +
+  return nw * wl + parse_misc_bytes() + 4 * parse_hl_words(n_max) + 4 * nbmax +
          (tallies > buckets ? tallies : buckets);
 }
 
@@ -753,7 +755,7 @@ __device__ void parse_epilogue_big(const ParseArgs& a, int n, int nbk, int64_t r
 template <int TM, int WIN>
 __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   constexpr int CH = WIN / 64;
-  using WL = WaveLds<WIN>;
+  using WL = WaveLds<WIN, lds_base<TM>()>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int l = lane();
   const int nw = (int)(blockDim.x >> 6);

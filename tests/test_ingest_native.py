@@ -175,7 +175,7 @@ def test_multi_job_shared_reads(ing, tmp_path):
         ing.pack_samples(jobs + [(str(tmp_path / "r1.fa"), str(tmp_path / "p3.paf"), str(reads))])
 
 
-def _fuzz_files(rng, tmp_path, interior, trailing):
+def _fuzz_files(rng, tmp_path, interior, trailing, paf_errors=False):
     """Random FASTA/PAF text: line lengths around the 64-byte blocks of the native
     scan, lower case, trailing whitespace, rare non-base bytes, blank lines,
     duplicate names in both files, records no PAF line names."""
@@ -201,7 +201,17 @@ def _fuzz_files(rng, tmp_path, interior, trailing):
         nm = names[int(rng.integers(len(names)))]
         qlen = int(rng.integers(1, 400))
         qs, qe = sorted(int(x) for x in rng.integers(-5, qlen + 5, size=2))
-        paf += paf_line(nm, qlen, qs, qe, "-" if rng.random() < 0.5 else "+", int(rng.integers(0, 5)), ":3")
+        line = paf_line(nm, qlen, qs, qe, "-" if rng.random() < 0.5 else "+", int(rng.integers(0, 5)), ":3",
+                        extra=str(rng.choice(["", "NM:i:3", "cs:Z::3", "tp:A:P\tcs:Z::3"])))
+        u = rng.random()
+        if u < 0.15:  # trailing whitespace, tabs included (rstrip() before split)
+            line = line[:-1] + str(rng.choice(["\t", " \t", "\t\t ", "\x0c"])) + "\n"
+        elif u < 0.25:  # a tag after the cs field, long enough to cross 64-byte blocks
+            line = line[:-1] + "\tzz:Z:" + "x" * int(rng.integers(0, 150)) + "\n"
+        paf += line
+    if paf_errors:  # lines the reference rejects: short, no cs tag, non-integer fields
+        paf += str(rng.choice(["a\t4\t0\n", "a\t4\t0\t4\t+\tref\t4\t0\t4\t4\t4\t60\n",
+                               paf_line("a", 4, 0, 4, "+", 0, ":4").replace("\t4\t0\t4\t", "\t4\tx\t4\t", 1)]))
     return _files(tmp_path, ">r\nACGTACGTACGT\n", paf, reads)
 
 
@@ -213,9 +223,9 @@ def test_fuzz_block_scan_and_name_table(ing, seed, tmp_path):
     the seeds; trailing whitespace (stripped, no error) in two thirds."""
     rng = np.random.default_rng(seed)
     interior = 0.08 if seed % 3 == 1 else 0.0
-    paths = _fuzz_files(rng, tmp_path, interior, 0.0 if seed % 3 == 2 else 0.15)
+    paths = _fuzz_files(rng, tmp_path, interior, 0.0 if seed % 3 == 2 else 0.15, paf_errors=seed % 4 == 3)
     nat = _same(ing, *paths)
-    if not interior:
+    if not interior and seed % 4 != 3:
         assert nat is not None and len(nat["tstart"]) > 20
     for n_threads in (1, 2, 5, 16):
         try:

@@ -332,6 +332,33 @@ def pack_sample(ref_path, paf_path, reads_path, native=True):
     return pack_sample_python(ref_path, paf_path, reads_path)
 
 
+def job_groups(jobs):
+    """Indices of (ref_path, paf_path, reads_path) jobs grouped by reads file, each
+    group in job order, groups in the order of their first job."""
+    groups = {}
+    for j, (_, _, reads) in enumerate(jobs):
+        groups.setdefault(os.fspath(reads), []).append(j)
+    return list(groups.values())
+
+
+def pack_group(jobs, native=True):
+    """Steps 1-3 for jobs that share ONE reads file (one scan of it) -> per job,
+    its packed dict or the :class:`IngestError` the reference raises for it
+    (not raised here); jobs the native parser declines take the Python path."""
+    out = [None] * len(jobs)
+    if native and jobs:
+        r = pack_samples_native([(ref, paf) for ref, paf, _ in jobs], jobs[0][2])
+        if r is not None:
+            out = list(r)
+    for j, (ref, paf, reads) in enumerate(jobs):
+        if out[j] is None:
+            try:
+                out[j] = pack_sample_python(ref, paf, reads)
+            except (IngestError, UnicodeDecodeError, OSError) as e:
+                out[j] = e
+    return out
+
+
 def pack_samples(jobs, native=True):
     """Steps 1-3 for (ref_path, paf_path, reads_path) jobs -> list of packed
     dicts, in job order.  Jobs sharing a reads file are ingested together (one

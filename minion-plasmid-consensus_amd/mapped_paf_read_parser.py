@@ -64,6 +64,61 @@ def build_parser():
     return p
 
 
+def _ingest_and_pileup(ingest, engine, jobs, args, tm):
+    """Steps 1-6 of every job.  Jobs sharing a reads file are ingested together
+    (one scan of it); a group's pileup runs on the device (a worker thread: the
+    native ingest and the HIP calls release the GIL) while the next group is
+    ingested.  Errors as the jobs would raise them in order: the first job
+    (in job order) the ingest rejects, else the first group's device error.
+    Returns the per-job call dicts, or None when --min_depth_factor is missing
+    (every file is still read first, as the reference does).  ``tm`` receives
+    the phase walls: ingest (all groups), device (what the ingest did not
+    hide)."""
+    import concurrent.futures as cf
+    mdf, gtf = args.MIN_DEPTH_FACTOR, args.GLOBAL_THRESHOLD_FACTOR
+    triples = [(ref, paf, reads) for ref, paf, reads, *_ in jobs]
+    groups = ingest.job_groups(triples)
+    packed, futs, t_ing = [None] * len(jobs), [], 0.0
+    with cf.ThreadPoolExecutor(max_workers=1) as dev:
+        for idx in groups:
+            t = time.perf_counter()
+            got = ingest.pack_group([triples[j] for j in idx])
+            t_ing += time.perf_counter() - t
+            for j, x in zip(idx, got):
+                packed[j] = x
+            ok = not any(isinstance(x, Exception) for x in got)
+            if ok:
+                for x in got:
+                    statprint("There were {} mapped reads.".format(x["n_alignments"]))
+            if ok and mdf is not None:
+                if not futs:
+                    statprint("Pileup and consensus on device {}...".format(args.device))
+                futs.append((idx, dev.submit(engine.pileup, got, mdf, 1.0 if gtf is None else gtf, args.device)))
+        t1 = time.perf_counter()
+        tm["ingest"] = t_ing
+        errs = [x for x in packed if isinstance(x, Exception)]
+        if errs:
+            for _, f in futs:  # let launched pileups finish before reporting
+                f.exception()
+            raise errs[0]
+        if mdf is None:
+            return None
+        results = [None] * len(jobs)
+        read0 = 0
+        for idx, f in futs:
+            try:
+                res = f.result()
+            except engine.DataError as e:  # read index in the launch of all jobs, as before
+                for _, g in futs:
+                    g.exception()
+                raise engine.DataError(e.flags, e.read + read0)
+            for j, r in zip(idx, res):
+                results[j] = r
+            read0 += sum(len(packed[j]["tstart"]) for j in idx)
+    tm["device"] = time.perf_counter() - t1
+    return results
+
+
 def main(argv=None, timings=None):
     """CLI entry.  ``timings`` (a dict, optional) receives the wall seconds of
     the phases: ingest, device (H2D + kernels + D2H), write."""
@@ -88,19 +143,10 @@ def main(argv=None, timings=None):
     try:
         for ref, paf, reads, *_ in jobs:
             statprint(f"Ingesting {paf} against {ref}...")
-        # jobs sharing a reads file are ingested together (one scan of it)
-        samples = ingest.pack_samples([(ref, paf, reads) for ref, paf, reads, *_ in jobs])
-        for s in samples:
-            statprint("There were {} mapped reads.".format(s["n_alignments"]))
-        t1 = time.perf_counter()
-        tm["ingest"] = t1 - t0
-        if args.MIN_DEPTH_FACTOR is None:
-            raise ingest.IngestError("TypeError: --min_depth_factor is required")  # max_depth*None (:338)
-        gtf = args.GLOBAL_THRESHOLD_FACTOR
-        statprint("Pileup and consensus on device {}...".format(args.device))
-        results = engine.pileup(samples, args.MIN_DEPTH_FACTOR, 1.0 if gtf is None else gtf, device=args.device)
-        tm["device"] = time.perf_counter() - t1
-        if gtf is None and any(len(r["count"]) or r["max_depth"] for r in results):
+        results = _ingest_and_pileup(ingest, engine, jobs, args, tm)
+        if results is None:  # (:338) max_depth * None, after every file was read
+            raise ingest.IngestError("TypeError: --min_depth_factor is required")
+        if args.GLOBAL_THRESHOLD_FACTOR is None and any(len(r["count"]) or r["max_depth"] for r in results):
             raise ingest.IngestError("TypeError: --global_threshold_factor is required")  # (:421)
     except (ingest.IngestError, engine.DataError, OSError, UnicodeDecodeError) as e:
         print("Error: {}".format(e), file=sys.stderr)

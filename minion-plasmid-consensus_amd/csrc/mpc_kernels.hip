@@ -1328,6 +1328,12 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
 // chunk's regions v, v + 16, ... (8 loads in flight per lane).
 // ---------------------------------------------------------------------------
 constexpr int kSubsWG = 32;  // parse workgroups per K_subs block, at most
+// K_subs blocks store their 16-bit tallies in a slab row each, reduced per
+// (sample, window) by K_subsum (instead of every block adding its ~4 n counters
+// into the same words with global atomics)
+#ifndef MPC_SUBS_SLAB
+#define MPC_SUBS_SLAB 1
+#endif
 struct SubsArgs {
   const int4* work;    // {sample, window, first parse workgroup, end}
   const int4* pwork;   // parse work table {sample, r0, r1, 0}
@@ -1335,6 +1341,7 @@ struct SubsArgs {
   const int64_t* cs_off; int64_t cs_base;
   const uint16_t* subev; const uint32_t* subev_cnt; int64_t subev_cap;
   const int32_t* n_of; const int32_t* gbase; uint32_t* sub;
+  uint32_t* slab;  // MPC_SUBS_SLAB: [K_subs block][kSubWin * 2] packed tallies
   int32_t nw_parse;
 };
 __global__ __launch_bounds__(1024) void K_subs(SubsArgs a) {
@@ -1364,10 +1371,59 @@ __global__ __launch_bounds__(1024) void K_subs(SubsArgs a) {
   }
   __syncthreads();
   const int64_t p0 = (int64_t)win * kSubWin, n = a.n_of[smp];
+  if (MPC_SUBS_SLAB) {  // the window's positions (< n), two words each, coalesced
+    uint32_t* row = a.slab + (int64_t)blockIdx.x * (kSubWin * 2);
+    const int nw2 = (int)(2 * (n - p0 < kSubWin ? n - p0 : kSubWin));
+    for (int j = threadIdx.x; j < nw2; j += blockDim.x) row[j] = cnt[j];
+    return;
+  }
   uint32_t* dst = a.sub + ((int64_t)a.gbase[smp] + p0) * 4;
   for (int j = threadIdx.x; j < kSubWin * 4; j += blockDim.x) {  // consecutive lanes, consecutive words
     const uint32_t x = (cnt[j >> 1] >> (16 * (j & 1))) & 0xffffu;
+#ifdef MPC_ABL_SUBS_NOFLUSH  // timing ablation only (wrong results): no flush
+    if (x == 0xfffffu) atomicAdd(dst + j, x);
+#else
     if (x && p0 + (j >> 2) < n) atomicAdd(dst + j, x);
+#endif
+  }
+}
+
+// K_subsum: per (sample, window, 256 slab words): the sum over the window's
+// K_subs blocks (4 groups of rows per thread column, 8 loads in flight each,
+// LDS reduce), stored into the substitution tallies (the only writer of a mode-3
+// window's words).  work: {sample, window, first block, end block}.
+constexpr int kSumCols = 256;
+__global__ __launch_bounds__(1024) void K_subsum(const int4* work, const uint32_t* slab, const int32_t* n_of,
+                                                 const int32_t* gbase, uint32_t* sub) {
+  __shared__ uint32_t part[4][kSumCols][2];
+  constexpr int kChunks = kSubWin * 2 / kSumCols;
+  const int4 wk = work[blockIdx.x / kChunks];
+  const int x = threadIdx.x & (kSumCols - 1), y = threadIdx.x / kSumCols;
+  const int64_t p0 = (int64_t)wk.y * kSubWin, n = n_of[wk.x];
+  const int nw2 = (int)(2 * (n - p0 < kSubWin ? n - p0 : kSubWin));
+  const int j = (int)(blockIdx.x % kChunks) * kSumCols + x;
+  uint32_t lo = 0, hi = 0;
+  if (j < nw2) {
+    for (int b0 = wk.z + y; b0 < wk.w; b0 += 4 * 8) {
+      uint32_t v[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int b = b0 + 4 * u;
+        v[u] = b < wk.w ? slab[(int64_t)b * (kSubWin * 2) + j] : 0u;
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) { lo += v[u] & 0xffffu; hi += v[u] >> 16; }
+    }
+  }
+  part[y][x][0] = lo;
+  part[y][x][1] = hi;
+  __syncthreads();
+  if (y == 0 && j < nw2) {
+    lo = part[0][x][0] + part[1][x][0] + part[2][x][0] + part[3][x][0];
+    hi = part[0][x][1] + part[1][x][1] + part[2][x][1] + part[3][x][1];
+    uint32_t* dst = sub + ((int64_t)gbase[wk.x] + p0) * 4 + 2 * j;  // word j: position j / 2, codes 2 (j & 1) + {0, 1}
+    dst[0] = lo;
+    dst[1] = hi;
   }
 }
 
@@ -2755,6 +2811,7 @@ struct mpc_plan {
   size_t ws_bytes = 0;
   uint8_t* ws = nullptr;
   std::vector<int32_t> work_parse, work_bc, work_sub;  // int4 records
+  std::vector<int32_t> work_subsum;                   // int4 {sample, window, first K_subs block, end}
   std::vector<int32_t> work_wave;                     // per parse workgroup: kMaxPW + 1 wave boundaries
   int32_t sub_wins = 0;                               // tally mode 3: substitution-event windows
   int64_t subev_cap = 0;
@@ -2769,7 +2826,7 @@ struct mpc_plan {
     // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
     B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
     B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_SROW, B_WPARSE, B_WBC, B_UNITS, B_RUNT,
-    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_COUNT
+    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_SUBSLAB, B_WSUBSUM, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -2848,7 +2905,11 @@ static void launch_subs(const mpc_plan* p, const Dev& d, hipStream_t st) {
   a.subev = at<uint16_t>(p, mpc_plan::B_SUBEV); a.subev_cnt = at<uint32_t>(p, mpc_plan::B_SUBCNT);
   a.subev_cap = p->subev_cap; a.n_of = d.n_of; a.gbase = d.gbase; a.sub = d.sub; a.nw_parse = p->parse_nw;
   a.wave_tab = at<const int32_t>(p, mpc_plan::B_WWAVE);
+  a.slab = at<uint32_t>(p, mpc_plan::B_SUBSLAB);
   hipLaunchKernelGGL(K_subs, dim3((unsigned)(p->work_sub.size() / 4)), dim3(1024), 0, st, a);
+  if (MPC_SUBS_SLAB)
+    hipLaunchKernelGGL(K_subsum, dim3((unsigned)(p->work_subsum.size() / 4 * (kSubWin * 2 / kSumCols))), dim3(1024), 0, st,
+                       at<const int4>(p, mpc_plan::B_WSUBSUM), (const uint32_t*)a.slab, d.n_of, d.gbase, d.sub);
 }
 static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
   const dim3 g(p->n_parse_wg), b(p->parse_nw * 64);
@@ -3183,9 +3244,13 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       const int kc = (int)std::max<int64_t>(1, std::min<int64_t>({(int64_t)kSubsWG, (pairs + 255) / 256,
                                                                    65535 / std::max<int64_t>(1, p->max_wg_reads)}));
       for (int s = 0; s < p->S; ++s)
-        for (int w = 0; w * (int64_t)kSubWin < p->ref_len[s]; ++w)
+        for (int w = 0; w * (int64_t)kSubWin < p->ref_len[s]; ++w) {
+          const int b0 = (int)(p->work_sub.size() / 4);
           for (int c = pw_begin[s]; c < pw_begin[s + 1]; c += kc)
             p->work_sub.insert(p->work_sub.end(), {s, w, c, std::min(c + kc, pw_begin[s + 1])});
+          const int b1 = (int)(p->work_sub.size() / 4);
+          if (b1 > b0) p->work_subsum.insert(p->work_subsum.end(), {s, w, b0, b1});
+        }
     }
     for (int s = 0; s < p->S; ++s) {
       const int nb = (int)((p->ref_len[s] + 1 + kBW - 1) / kBW);
@@ -3269,6 +3334,8 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_WSUB, (int64_t)p->work_sub.size(), 4);
   set(mpc_plan::B_BKCUR, p->tally_mode == 4 ? (int64_t)p->n_parse_wg * p->nbmax : 0, 4);
   set(mpc_plan::B_WWAVE, (int64_t)p->work_wave.size(), 4);
+  set(mpc_plan::B_SUBSLAB, MPC_SUBS_SLAB ? (int64_t)(p->work_sub.size() / 4) * kSubWin * 2 : 0, 4);
+  set(mpc_plan::B_WSUBSUM, (int64_t)p->work_subsum.size(), 4);
   size_t o = 0;
   for (int b = 0; b < mpc_plan::B_COUNT; ++b) {
     o = (o + 255) & ~(size_t)255;
@@ -3341,6 +3408,9 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
                      hipMemcpyHostToDevice));
   if (!p->work_sub.empty())
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WSUB), p->work_sub.data(), 4 * p->work_sub.size(), hipMemcpyHostToDevice));
+  if (!p->work_subsum.empty())
+    HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WSUBSUM), p->work_subsum.data(), 4 * p->work_subsum.size(),
+                     hipMemcpyHostToDevice));
   HIPCHK(hipFuncSetAttribute(parse_kernel(p->tally_mode, p->parse_win), hipFuncAttributeMaxDynamicSharedMemorySize,
                              p->parse_lds));
   p->bound = true;

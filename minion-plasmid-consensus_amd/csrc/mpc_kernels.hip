@@ -2577,7 +2577,11 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
     const int64_t w0 = s_w0[side];
     for (int k = tid; k < kWinRows * 4; k += blockDim.x) {
       const uint32_t v = win[side][(k >> 2) * 5 + (k & 3)];
+#ifdef MPC_ABL_FLANK_NOFLUSH  // timing ablation only (wrong results): no window flush
+      if (v == 0xfffffffu) atomicAdd(a.rows + w0 * 4 + k, v);
+#else
       if (v) atomicAdd(a.rows + w0 * 4 + k, v);
+#endif
     }
   }
   if (lerr) {

@@ -174,7 +174,7 @@ def e2e_cli(pkg, cfg, reps=2):
         return {"value": aligned / best["wall"], "unit": "aligned bases/s", "wall_s": best["wall"],
                 "wall_s_first": runs[0]["wall"], "aligned_bases": aligned, "input_bytes": in_bytes,
                 "output_files": n_files, "output_bytes": out_bytes,
-                "phases_s": {k: round(best[k], 4) for k in ("ingest", "device", "write")},
+                "phases_s": {k: round(best[k], 4) for k in ("setup", "ingest", "device", "write", "main") if k in best},
                 "write_frac": best["write"] / best["wall"],
                 "what": f"{cfg} files, {len(argv) // 7} job(s) in ONE CLI call (--job each), {n_files} output files; "
                         "CLI main(): native ingest of ref/PAF/reads FASTA + H2D + plan + kernels + D2H + "

@@ -670,10 +670,11 @@ void* out_alloc(size_t n) {
   *reinterpret_cast<OutHeader*>(a) = OutHeader{kMagicMalloc, a, n + 64};
   return a + 64;
 }
-void out_free(void* p) {
+// frees p; a mapping is appended to *maps instead (unmapped off the caller's clock)
+void out_free(void* p, std::vector<std::pair<void*, size_t>>* maps) {
   if (!p) return;
   const OutHeader h = *reinterpret_cast<const OutHeader*>(static_cast<uint8_t*>(p) - 64);
-  if (h.magic == kMagicMap) munmap(h.base, h.len);
+  if (h.magic == kMagicMap) maps->emplace_back(h.base, h.len);
   else free(h.base);
 }
 
@@ -750,8 +751,17 @@ int mpc_ingest_version(void) { return 3; }  // 3: + mpc_ingest_multi; 2: + mpc_w
 
 void mpc_ingest_free(mpc_ingest_out* o) {
   if (!o) return;
-  out_free(o->ref); out_free(o->cs); out_free(o->cs_off); out_free(o->tstart); out_free(o->up); out_free(o->up_off);
-  out_free(o->down); out_free(o->down_off); out_free(o->aligned);
+  std::vector<std::pair<void*, size_t>> maps;
+  for (void* b : {(void*)o->ref, (void*)o->cs, (void*)o->cs_off, (void*)o->tstart, (void*)o->up, (void*)o->up_off,
+                  (void*)o->down, (void*)o->down_off, (void*)o->aligned})
+    out_free(b, &maps);
+  if (!maps.empty()) {  // a GB of output pages: unmapped by a detached thread
+    try {
+      std::thread([maps] { for (const auto& m : maps) munmap(m.first, m.second); }).detach();
+    } catch (...) {
+      for (const auto& m : maps) munmap(m.first, m.second);
+    }
+  }
   o->ref = o->cs = o->up = o->down = nullptr;
   o->cs_off = o->tstart = o->up_off = o->down_off = o->aligned = nullptr;
 }

@@ -122,6 +122,7 @@ def _ingest_and_pileup(ingest, engine, jobs, args, tm):
 def main(argv=None, timings=None):
     """CLI entry.  ``timings`` (a dict, optional) receives the wall seconds of
     the phases: ingest, device (H2D + kernels + D2H), write."""
+    t_main = time.perf_counter()
     args = build_parser().parse_args(argv)
     tm = timings if timings is not None else {}
     pkg = _pkg()
@@ -140,6 +141,7 @@ def main(argv=None, timings=None):
         [(args.REF, args.PAF, args.READS, args.consensus, args.chromat, args.accuracies)]
     jobs += [(r, p, args.READS, c, ch, a) for r, p, c, ch, a in args.also] + [tuple(j) for j in args.job]
     t0 = time.perf_counter()
+    tm["setup"] = t0 - t_main
     try:
         for ref, paf, reads, *_ in jobs:
             statprint(f"Ingesting {paf} against {ref}...")
@@ -170,6 +172,7 @@ def main(argv=None, timings=None):
             print("Error: {}".format(e), file=sys.stderr)
             return 1
     statprint("Done.")
+    tm["main"] = time.perf_counter() - t_main
     return 0
 
 

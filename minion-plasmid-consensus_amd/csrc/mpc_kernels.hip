@@ -1357,17 +1357,30 @@ __global__ __launch_bounds__(1024) void K_subs(SubsArgs a) {
     const int64_t ra = a.wave_tab[(int64_t)pw * (kMaxCh + 1) + ww];  // the chunk's first read
     const int c = (int)a.subev_cnt[((int64_t)pw * kMaxCh + ww) * kMaxSubWins + win];
     const uint16_t* src = a.subev + (int64_t)win * a.subev_cap + (a.cs_off[ra] - a.cs_base) / 3 + 2 * ra;
-    for (int e0 = 0; e0 < c; e0 += 8 * 64) {
-      uint32_t ev[8];
+    auto tally = [&](uint32_t ev) { atomicAdd(&cnt[ev >> 1], 1u << (16 * (ev & 1u))); };
+    // 16-byte loads (8 events per lane each, 4 in flight): the region's events up
+    // to the first 16-byte boundary and after the last whole group one per lane
+    const int head = min(c, (int)(((16u - ((uint32_t)(uintptr_t)src & 15u)) & 15u) >> 1));
+    if (l < head) tally(src[l]);
+    const uint4* body = reinterpret_cast<const uint4*>(src + head);
+    const int ng = (c - head) >> 3;
+    for (int q0 = 0; q0 < ng; q0 += 4 * 64) {
+      uint4 g[4];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int e = e0 + l + 64 * u;
-        ev[u] = e < c ? (uint32_t)src[e] : ~0u;
+      for (int u = 0; u < 4; ++u) {
+        const int q = q0 + l + 64 * u;
+        g[u] = q < ng ? body[q] : make_uint4(0u, 0u, 0u, 0u);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u)
-        if (ev[u] != ~0u) atomicAdd(&cnt[ev[u] >> 1], 1u << (16 * (ev[u] & 1u)));
+      for (int u = 0; u < 4; ++u) {
+        if (q0 + l + 64 * u >= ng) continue;
+        const uint32_t w4[4] = {g[u].x, g[u].y, g[u].z, g[u].w};
+#pragma unroll
+        for (int h = 0; h < 4; ++h) { tally(w4[h] & 0xffffu); tally(w4[h] >> 16); }
+      }
     }
+    const int t0 = head + 8 * ng;
+    if (t0 + l < c) tally(src[t0 + l]);  // (< 8 events)
   }
   __syncthreads();
   const int64_t p0 = (int64_t)win * kSubWin, n = a.n_of[smp];
@@ -1393,9 +1406,10 @@ __global__ __launch_bounds__(1024) void K_subs(SubsArgs a) {
 // LDS reduce), stored into the substitution tallies (the only writer of a mode-3
 // window's words).  work: {sample, window, first block, end block}.
 constexpr int kSumCols = 256;
-__global__ __launch_bounds__(1024) void K_subsum(const int4* work, const uint32_t* slab, const int32_t* n_of,
-                                                 const int32_t* gbase, uint32_t* sub) {
-  __shared__ uint32_t part[4][kSumCols][2];
+template <int RG>  // row groups: 4 when windows have many slab rows (C3: 256), else 1 (C5: ~5)
+__global__ __launch_bounds__(kSumCols * RG) void K_subsum(const int4* work, const uint32_t* slab, const int32_t* n_of,
+                                                          const int32_t* gbase, uint32_t* sub) {
+  __shared__ uint32_t part[RG][kSumCols][2];
   constexpr int kChunks = kSubWin * 2 / kSumCols;
   const int4 wk = work[blockIdx.x / kChunks];
   const int x = threadIdx.x & (kSumCols - 1), y = threadIdx.x / kSumCols;
@@ -1404,11 +1418,11 @@ __global__ __launch_bounds__(1024) void K_subsum(const int4* work, const uint32_
   const int j = (int)(blockIdx.x % kChunks) * kSumCols + x;
   uint32_t lo = 0, hi = 0;
   if (j < nw2) {
-    for (int b0 = wk.z + y; b0 < wk.w; b0 += 4 * 8) {
+    for (int b0 = wk.z + y; b0 < wk.w; b0 += RG * 8) {
       uint32_t v[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int b = b0 + 4 * u;
+        const int b = b0 + RG * u;
         v[u] = b < wk.w ? slab[(int64_t)b * (kSubWin * 2) + j] : 0u;
       }
 #pragma unroll
@@ -1419,8 +1433,10 @@ __global__ __launch_bounds__(1024) void K_subsum(const int4* work, const uint32_
   part[y][x][1] = hi;
   __syncthreads();
   if (y == 0 && j < nw2) {
-    lo = part[0][x][0] + part[1][x][0] + part[2][x][0] + part[3][x][0];
-    hi = part[0][x][1] + part[1][x][1] + part[2][x][1] + part[3][x][1];
+    lo = 0;
+    hi = 0;
+#pragma unroll
+    for (int r = 0; r < RG; ++r) { lo += part[r][x][0]; hi += part[r][x][1]; }
     uint32_t* dst = sub + ((int64_t)gbase[wk.x] + p0) * 4 + 2 * j;  // word j: position j / 2, codes 2 (j & 1) + {0, 1}
     dst[0] = lo;
     dst[1] = hi;
@@ -1681,7 +1697,9 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
 #pragma unroll
     for (int u = 0; u < kRegE; ++u) e[u] = s0 + 64 * u + l < s1 ? pool[s0 + 64 * u + l] : 0u;
     __syncthreads();  // every wave holds its entries before the first scatter
+#ifndef MPC_ABL_RSORT_NOPASS  // timing ablation only (wrong order): no sort passes
     for (int p = 0; p < passes; ++p) rsort_reg_pass(e, s0, s1, sb + 8 * p, pool, wc, hb, p + 1 < passes);
+#endif
     const uint32_t im = (1u << sb) - 1u;  // (sb <= 15 here)
     for (int64_t i0 = 0; i0 < M; i0 += 4 * kRS) {
       uint32_t x[4];
@@ -1689,7 +1707,11 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
       for (int u = 0; u < 4; ++u) { const int64_t i = i0 + tid + u * kRS; x[u] = i < M ? pool[i] : 0u; }
       int32_t vv[4];
 #pragma unroll
+#ifdef MPC_ABL_RSORT_NOVALS  // timing ablation only (wrong values): no value gather
+      for (int u = 0; u < 4; ++u) vv[u] = (int32_t)(x[u] & im) & 0;
+#else
       for (int u = 0; u < 4; ++u) { const int64_t i = i0 + tid + u * kRS; vv[u] = i < M ? d.vals_tmp[x[u] & im] : 0; }
+#endif
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t i = i0 + tid + u * kRS;
@@ -2558,7 +2580,11 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
       // 32-bit: rows < row_cap < 2^31, a block's flank bytes < 2^31
       const int cn32 = (int)cn, c032 = (int)c0;
       const int32_t w032 = w0 >= 0 ? (int32_t)w0 : -(1 << 30);  // no window: never a hit
+#ifdef MPC_ABL_FLANK_NOBYTES  // timing ablation only (wrong results): no per-byte tallies
+      for (int x = tid; x < 0; x += blockDim.x) {
+#else
       for (int x = tid; x < cn32; x += blockDim.x) {
+#endif
         const uint32_t word = bm[x >> 5];
         const int o = wpre[x >> 5] + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
         const int32_t rw = t_row[o];
@@ -2816,6 +2842,7 @@ struct mpc_plan {
   uint8_t* ws = nullptr;
   std::vector<int32_t> work_parse, work_bc, work_sub;  // int4 records
   std::vector<int32_t> work_subsum;                   // int4 {sample, window, first K_subs block, end}
+  int subsum_rows = 0;                                // most K_subs blocks of one (sample, window)
   std::vector<int32_t> work_wave;                     // per parse workgroup: kMaxPW + 1 wave boundaries
   int32_t sub_wins = 0;                               // tally mode 3: substitution-event windows
   int64_t subev_cap = 0;
@@ -2911,9 +2938,15 @@ static void launch_subs(const mpc_plan* p, const Dev& d, hipStream_t st) {
   a.wave_tab = at<const int32_t>(p, mpc_plan::B_WWAVE);
   a.slab = at<uint32_t>(p, mpc_plan::B_SUBSLAB);
   hipLaunchKernelGGL(K_subs, dim3((unsigned)(p->work_sub.size() / 4)), dim3(1024), 0, st, a);
-  if (MPC_SUBS_SLAB)
-    hipLaunchKernelGGL(K_subsum, dim3((unsigned)(p->work_subsum.size() / 4 * (kSubWin * 2 / kSumCols))), dim3(1024), 0, st,
-                       at<const int4>(p, mpc_plan::B_WSUBSUM), (const uint32_t*)a.slab, d.n_of, d.gbase, d.sub);
+  if (MPC_SUBS_SLAB) {
+    const dim3 g((unsigned)(p->work_subsum.size() / 4 * (kSubWin * 2 / kSumCols)));
+    if (p->subsum_rows > 8)
+      hipLaunchKernelGGL(K_subsum<4>, g, dim3(4 * kSumCols), 0, st, at<const int4>(p, mpc_plan::B_WSUBSUM),
+                         (const uint32_t*)a.slab, d.n_of, d.gbase, d.sub);
+    else
+      hipLaunchKernelGGL(K_subsum<1>, g, dim3(kSumCols), 0, st, at<const int4>(p, mpc_plan::B_WSUBSUM),
+                         (const uint32_t*)a.slab, d.n_of, d.gbase, d.sub);
+  }
 }
 static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
   const dim3 g(p->n_parse_wg), b(p->parse_nw * 64);
@@ -3254,6 +3287,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
             p->work_sub.insert(p->work_sub.end(), {s, w, c, std::min(c + kc, pw_begin[s + 1])});
           const int b1 = (int)(p->work_sub.size() / 4);
           if (b1 > b0) p->work_subsum.insert(p->work_subsum.end(), {s, w, b0, b1});
+          p->subsum_rows = std::max(p->subsum_rows, b1 - b0);
         }
     }
     for (int s = 0; s < p->S; ++s) {

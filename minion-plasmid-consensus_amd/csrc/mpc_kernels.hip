@@ -2574,27 +2574,39 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
         }
       }
       __syncthreads();
-      // consecutive lanes take consecutive bytes: a flank's bytes go to
+      // every thread takes 4 consecutive bytes (one owner lookup, one stage
+      // dword); consecutive lanes, consecutive dwords: a flank's bytes go to
       // consecutive rows, so a wave's (rare) global atomics cover a few
       // contiguous segments instead of one scattered row per lane
       // 32-bit: rows < row_cap < 2^31, a block's flank bytes < 2^31
       const int cn32 = (int)cn, c032 = (int)c0;
       const int32_t w032 = w0 >= 0 ? (int32_t)w0 : -(1 << 30);  // no window: never a hit
+      const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
 #ifdef MPC_ABL_FLANK_NOBYTES  // timing ablation only (wrong results): no per-byte tallies
-      for (int x = tid; x < 0; x += blockDim.x) {
+      for (int x4 = 4 * tid; x4 < 0; x4 += 4 * (int)blockDim.x) {
 #else
-      for (int x = tid; x < cn32; x += blockDim.x) {
+      for (int x4 = 4 * tid; x4 < cn32; x4 += 4 * (int)blockDim.x) {
 #endif
-        const uint32_t word = bm[x >> 5];
-        const int o = wpre[x >> 5] + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
-        const int32_t rw = t_row[o];
-        if (rw < 0) continue;
-        const int32_t row = rw + (c032 + x - t_start[o]);
-        const int code = code_exact(stage[x + sh0]);
-        if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
-        const uint32_t wr = (uint32_t)(row - w032);
-        if (wr < (uint32_t)kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
-        else atomicAdd(a.rows + (int64_t)row * 4 + code, 1u);
+        const uint32_t word = bm[x4 >> 5];  // (the 4 bytes share a bitmap word)
+        const int ob = wpre[x4 >> 5];
+        const int q = x4 + sh0;             // stage offset (+16 padding: the second dword is in bounds)
+        const uint32_t by = __builtin_amdgcn_alignbyte(s32[(q >> 2) + 1], s32[q >> 2], (uint32_t)(q & 3));
+        int o_prev = -1;
+        int32_t rw = -1, ts = 0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int x = x4 + k;
+          if (x >= cn32) break;
+          const int o = ob + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
+          if (o != o_prev) { rw = t_row[o]; ts = t_start[o]; o_prev = o; }
+          if (rw < 0) continue;
+          const int32_t row = rw + (c032 + x - ts);
+          const int code = code_exact((by >> (8 * k)) & 0xffu);
+          if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
+          const uint32_t wr = (uint32_t)(row - w032);
+          if (wr < (uint32_t)kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
+          else atomicAdd(a.rows + (int64_t)row * 4 + code, 1u);
+        }
       }
     }
   }

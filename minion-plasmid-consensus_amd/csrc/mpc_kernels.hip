@@ -2452,10 +2452,19 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
   __shared__ int32_t s_w[FR / 64], s_nne, s_cbase;
   if (a.status[MPC_ST_FLAGS] & (DE_CAP | DE_INTERNAL)) return;
   const int tid = threadIdx.x, l = lane(), w = tid >> 6;
-  const int64_t r0 = (int64_t)blockIdx.x * FR;
+  const int64_t tot = a.status[MPC_ST_ROWS_NEEDED];
+  for (int k = tid; k < 2 * kWinRows * 5; k += blockDim.x) (&win[0][0])[k] = 0;
+  uint32_t lerr = 0;
+  int64_t lread = INT64_MAX;
+  // chunks of FR reads, grid-stride: the LDS windows (placed by the block's
+  // first chunk) are flushed once per block, not once per chunk -- the flush
+  // atomics of every block land on the same rows (the hot gaps)
+  const int64_t nchunks = (a.N + FR - 1) / FR;
+#pragma unroll 1
+  for (int64_t ck = blockIdx.x; ck < nchunks; ck += gridDim.x) {
+  const int64_t r0 = ck * FR;
   const int64_t r1 = r0 + FR < a.N ? r0 + FR : a.N;
   const int nr = (int)(r1 - r0);
-  const int64_t tot = a.status[MPC_ST_ROWS_NEEDED];
   const int64_t r = r0 + tid;
   const bool live = tid < nr;
   // per-read records: flank byte ranges and the row of byte 0 of each flank
@@ -2466,7 +2475,6 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
     off[0] = a.up_off[r]; end[0] = a.up_off[r + 1];
     off[1] = a.down_off[r]; end[1] = a.down_off[r + 1];
   }
-  for (int k = tid; k < 2 * kWinRows * 5; k += blockDim.x) (&win[0][0])[k] = 0;
   int64_t rs[2] = {-1, -1};
   int32_t gap[2] = {-1, -1};
   if (live) {
@@ -2493,16 +2501,15 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
       gap[1] = (int32_t)g;
     }
   }
+  __syncthreads();  // the previous chunk is done with the shared tables
   s_gap[0][tid] = gap[0];
   s_gap[1][tid] = gap[1];
   __syncthreads();
-  if (tid < 2) {  // LDS window: rows of the gap most of the block's reads use (vote of 3 reads)
+  if (tid < 2 && ck == blockIdx.x) {  // LDS window: rows of the gap most of the first chunk's reads use (vote of 3)
     const int32_t x = s_gap[tid][0], y = s_gap[tid][nr / 2], z = s_gap[tid][nr - 1];
     const int32_t gw = (x == y || x == z) ? x : y;
     s_w0[tid] = gw >= 0 ? (int64_t)a.row_base[gw] : (int64_t)INT32_MIN;
   }
-  uint32_t lerr = 0;
-  int64_t lread = INT64_MAX;
 #pragma unroll 1
   for (int side = 0; side < 2; ++side) {
     const uint8_t* src = side ? a.down : a.up;
@@ -2610,6 +2617,7 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
       }
     }
   }
+  }  // chunks
   __syncthreads();
   for (int side = 0; side < 2; ++side) {
     const int64_t w0 = s_w0[side];
@@ -3011,9 +3019,12 @@ static void launch_left(const mpc_plan* p, const Dev& d, hipStream_t st) {
 }
 static int64_t ins_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 512)); }
 static int flank_reads(const mpc_plan* p) { return (p->N + kFR - 1) / kFR < 256 ? kFRSmall : kFR; }
+// K_flank blocks: chunks of flank_reads reads, at most about four resident
+// blocks per CU (each further chunk of a block shares its window flush)
+constexpr int64_t kFlankBlocksMax = 1024;
 static int64_t flank_grid(const mpc_plan* p) {
   const int fr = flank_reads(p);
-  return std::max<int64_t>(1, (p->N + fr - 1) / fr);
+  return std::max<int64_t>(1, std::min<int64_t>(kFlankBlocksMax, (p->N + fr - 1) / fr));
 }
 
 static InsArgs ins_args(const mpc_plan* p, const Dev& d) {

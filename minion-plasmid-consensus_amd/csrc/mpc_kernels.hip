@@ -169,6 +169,8 @@ struct Dev {  // device-side views of the plan for the small kernels (passed by 
   int32_t* maxR;
   uint32_t* keys_in; int32_t* vals_in; uint32_t* keys_out; int32_t* vals_out;
   uint32_t* keys_tmp; int32_t* vals_tmp; int32_t* bcnt; int32_t* bpre;  // K_rsplit -> K_rsort
+  int32_t* gcnt; int32_t* kslot;     // multi-workgroup sort: [G+1] mixed events per gap, [N] slot in its gap
+  int32_t* rsflag;                   // [4] its path word, scan partials follow (K_rscan)
   int32_t* rlen;                     // [Ng] downstream length by global read
   int32_t* rpos;                     // [N] local read -> position of its mixed RIGHT event in the sorted list
   int32_t* right_start;              // [G+1] mixed RIGHT events (all shards) with gap < g
@@ -1450,6 +1452,7 @@ __global__ __launch_bounds__(kSumCols * RG) void K_subsum(const int4* work, cons
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ bool has_left(const uint32_t* bm, int64_t g) { return (bm[g >> 5] >> (g & 31)) & 1u; }
 
+__device__ __forceinline__ bool l_is(int j) { return lane() == j; }
 __device__ __forceinline__ void rsplit_block(const Dev& d, int64_t b) {
   __shared__ int64_t s_key;
   __shared__ int32_t s_val;
@@ -1484,6 +1487,18 @@ __device__ __forceinline__ void rsplit_block(const Dev& d, int64_t b) {
     const int64_t o = b * blockDim.x + wpre + inc - 1;
     d.keys_in[o] = (uint32_t)g;
     d.vals_in[o] = (int32_t)rg;
+  }
+  if (d.gcnt) {  // multi-workgroup sort: the event's slot within its gap (any order), one atomic per gap per wave
+    for (uint64_t act = ballot(mixed); act;) {
+      const int lead = __ffsll((unsigned long long)act) - 1;
+      const int32_t gl = __builtin_amdgcn_readlane((int)g, lead);
+      const uint64_t same = ballot(mixed && (int32_t)g == gl);
+      int32_t base = 0;
+      if (l_is(lead)) base = atomicAdd(d.gcnt + gl, __popcll(same));
+      base = __builtin_amdgcn_readlane(base, lead);
+      if (mixed && (int32_t)g == gl) d.kslot[b * blockDim.x + wpre + inc - 1] = base + lanes_below(same);
+      act &= ~same;
+    }
   }
   if (threadIdx.x == blockDim.x - 1) d.bcnt[b] = wpre + inc;
   block_atomic_max(d.maxR, g < 0 ? 0 : g, len, in && g >= 0 && !mixed, &s_key, &s_val);
@@ -1634,6 +1649,7 @@ __device__ __forceinline__ void rsort_reg_pass(uint32_t (&e)[kRegE], int64_t s0,
 }
 
 __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t end_bit) {
+  if (d.rsflag && d.rsflag[0] == 1) return;  // the multi-workgroup path sorted them
   __shared__ uint32_t pool[4 * kSortLds];  // LDS path: keys and values, two buffers each; register path: one buffer
   uint32_t (*lk)[kSortLds] = reinterpret_cast<uint32_t (*)[kSortLds]>(pool);
   int32_t (*lv)[kSortLds] = reinterpret_cast<int32_t (*)[kSortLds]>(pool + 2 * kSortLds);
@@ -1792,6 +1808,115 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
                  src_out ? d.vals_tmp : d.vals_out, 8 * p, s0, s1, wc, hb);
     }
   }
+}
+
+// ---------------------------------------------------------------------------
+// Multi-workgroup sort of the mixed RIGHT events (many reads: K_rsort's one
+// workgroup took 88 us at C3's 19k events, all of it latency).  K_rsplit gave
+// every event a slot within its gap (atomics: any order); K_rscan scans the
+// per-gap counts (two launches: block sums, then block scans with the sum of
+// the blocks before), K_rscatter puts every event at rsl[gap] + slot, and
+// K_rsegsort restores read order inside each gap (a wave's bitonic sort of up
+// to 64 reads).  A gap with more than 64 events, or few events overall, sends
+// the launch to K_rsort instead (path word rsflag[0]: 1 = this path).
+// ---------------------------------------------------------------------------
+constexpr int64_t kRsortMultiBlocks = 512;      // K_rsplit blocks (of 1024 reads) above which the plan takes this path
+constexpr int kScanPer = 8;                     // gaps per thread of K_rscan
+constexpr int kScanBlk = 1024 * kScanPer;       // gaps per K_rscan block
+constexpr int kSegMax = 64;
+
+__global__ __launch_bounds__(1024) void K_rscan1(Dev d) {
+  __shared__ int32_t s_s[16], s_m[16];
+  const int64_t g0 = (int64_t)blockIdx.x * kScanBlk + (int64_t)threadIdx.x * kScanPer;
+  int32_t sum = 0, mx = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    const int32_t c = g0 + k <= d.G ? d.gcnt[g0 + k] : 0;
+    sum += c;
+    mx = c > mx ? c : mx;
+  }
+  sum = wave_sum(sum);
+  for (int o = 32; o; o >>= 1) { const int32_t y = __shfl_xor(mx, o, 64); mx = y > mx ? y : mx; }
+  const int w = threadIdx.x >> 6;
+  if (lane() == 0) { s_s[w] = sum; s_m[w] = mx; }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int32_t t = 0, m = 0;
+    for (int k = 0; k < 16; ++k) { t += s_s[k]; m = s_m[k] > m ? s_m[k] : m; }
+    d.rsflag[4 + 2 * blockIdx.x] = t;
+    d.rsflag[5 + 2 * blockIdx.x] = m;
+  }
+}
+
+__global__ __launch_bounds__(1024) void K_rscan2(Dev d, int32_t nblk_scan) {
+  __shared__ int32_t s_w[16];
+  __shared__ int32_t s_pre, s_tot, s_max;
+  const int tid = threadIdx.x, l = lane(), w = tid >> 6;
+  if (tid < 64) {  // blocks before this one, and the totals
+    int32_t pre = 0, tot = 0, mx = 0;
+    for (int k = tid; k < nblk_scan; k += 64) {
+      const int32_t c = d.rsflag[4 + 2 * k], m = d.rsflag[5 + 2 * k];
+      tot += c;
+      if (k < (int)blockIdx.x) pre += c;
+      mx = m > mx ? m : mx;
+    }
+    pre = wave_sum(pre);
+    tot = wave_sum(tot);
+    for (int o = 32; o; o >>= 1) { const int32_t y = __shfl_xor(mx, o, 64); mx = y > mx ? y : mx; }
+    if (tid == 0) { s_pre = pre; s_tot = tot; s_max = mx; }
+  }
+  __syncthreads();
+  const int64_t g0 = (int64_t)blockIdx.x * kScanBlk + (int64_t)tid * kScanPer;
+  int32_t c[kScanPer], sum = 0;
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) { c[k] = g0 + k <= d.G ? d.gcnt[g0 + k] : 0; sum += c[k]; }
+  const int inc = wave_scan_i32(sum);
+  if (l == 63) s_w[w] = inc;
+  __syncthreads();
+  int32_t run = s_pre + inc - sum;
+  for (int k = 0; k < w; ++k) run += s_w[k];
+#pragma unroll
+  for (int k = 0; k < kScanPer; ++k) {
+    if (g0 + k <= d.G) d.rsl[g0 + k] = run;  // (K_rstart writes the same values again)
+    run += c[k];
+  }
+  if (blockIdx.x == 0 && tid == 0) {
+    const bool multi = s_tot > kSortLds && s_max <= kSegMax;
+    d.rsflag[0] = multi ? 1 : 0;
+    if (multi) d.status[MPC_ST_MIXED] = (uint32_t)s_tot;
+  }
+}
+
+__global__ __launch_bounds__(kRS) void K_rscatter(Dev d) {
+  if (d.rsflag[0] != 1) return;
+  const int64_t b = blockIdx.x;
+  const int c = d.bcnt[b];
+  if ((int)threadIdx.x >= c) return;
+  const int64_t o = b * kRS + threadIdx.x;
+  const uint32_t g = d.keys_in[o];
+  const int64_t pos = (int64_t)d.rsl[g] + d.kslot[o];
+  d.keys_out[pos] = g;
+  d.vals_out[pos] = d.vals_in[o];
+}
+
+// one wave per gap: its (<= 64) reads in ascending order, bitonic over the lanes
+__global__ __launch_bounds__(256) void K_rsegsort(Dev d) {
+  if (d.rsflag[0] != 1) return;
+  const int64_t g = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (g > d.G) return;
+  const int32_t c = d.gcnt[g];
+  if (c < 2) return;  // (wave-uniform)
+  const int l = lane();
+  const int64_t a0 = d.rsl[g];
+  int32_t v = l < c ? d.vals_out[a0 + l] : INT32_MAX;
+  for (int k = 2; k <= 64; k <<= 1) {
+    for (int j = k >> 1; j > 0; j >>= 1) {
+      const int32_t y = __shfl_xor(v, j, 64);
+      const bool up = (l & k) == 0, low = (l & j) == 0;
+      v = (low == up) ? (v < y ? v : y) : (v > y ? v : y);
+    }
+  }
+  if (l < c) d.vals_out[a0 + l] = v;
 }
 
 // rsl[g] = #mixed RIGHT events of this shard with gap < g; rpos[local read] =
@@ -2858,6 +2983,7 @@ struct mpc_plan {
   int32_t overrides = 0;  // MPC_OVR_* (experiment builds only)
   uint32_t sentinel = 0;
   int end_bit = 0;
+  bool rsort_multi = false;  // mixed RIGHT events sorted by K_rscan / K_rscatter / K_rsegsort (many reads)
   size_t ws_bytes = 0;
   uint8_t* ws = nullptr;
   std::vector<int32_t> work_parse, work_bc, work_sub;  // int4 records
@@ -2877,7 +3003,7 @@ struct mpc_plan {
     // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
     B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
     B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_SROW, B_WPARSE, B_WBC, B_UNITS, B_RUNT,
-    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_SUBSLAB, B_WSUBSUM, B_COUNT
+    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_SUBSLAB, B_WSUBSUM, B_GCNT, B_KSLOT, B_RSFLAG, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -2904,6 +3030,9 @@ Dev mpc_plan::dev() const {
   d.keys_out = at<uint32_t>(this, B_KOUT); d.vals_out = at<int32_t>(this, B_VOUT);
   d.keys_tmp = at<uint32_t>(this, B_KTMP); d.vals_tmp = at<int32_t>(this, B_VTMP);
   d.bcnt = at<int32_t>(this, B_BCNT); d.bpre = at<int32_t>(this, B_BPRE);
+  d.gcnt = rsort_multi ? at<int32_t>(this, B_GCNT) : nullptr;
+  d.kslot = rsort_multi ? at<int32_t>(this, B_KSLOT) : nullptr;
+  d.rsflag = rsort_multi ? at<int32_t>(this, B_RSFLAG) : nullptr;
   d.rlen = at<int32_t>(this, B_RLEN); d.rpos = at<int32_t>(this, B_RPOS); d.right_start = at<int32_t>(this, B_RSTART);
   d.rsl = at<int32_t>(this, B_RSLOC); d.roff = at<int32_t>(this, B_ROFF); d.rcnt = at<int32_t>(this, B_RCNT);
   d.rcnt_all = at<int32_t>(this, B_RCNTALL); d.shard = shard; d.n_shards = n_shards;
@@ -3359,6 +3488,12 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_VTMP, N, 4);
   set(mpc_plan::B_BCNT, nrb + 1, 4);
   set(mpc_plan::B_BPRE, nrb + 1, 4);
+  // K_rsort's one workgroup gathers and sorts in time that grows with the read
+  // blocks (C3, 977 blocks: 88 us): many reads take the multi-workgroup path
+  p->rsort_multi = nrb > kRsortMultiBlocks;
+  set(mpc_plan::B_GCNT, p->rsort_multi ? G + 1 : 0, 4);
+  set(mpc_plan::B_KSLOT, p->rsort_multi ? nrb * (int64_t)kRS : 0, 4);
+  set(mpc_plan::B_RSFLAG, p->rsort_multi ? 4 + 2 * ((G + 1 + kScanBlk - 1) / kScanBlk) : 0, 4);
   set(mpc_plan::B_RLEN, Ng, 4);
   set(mpc_plan::B_RPOS, N > 0 ? N : 1, 4);
   set(mpc_plan::B_RSTART, G + 1, 4);
@@ -3504,6 +3639,20 @@ int mpc_plan_buffer(const mpc_plan* p, int which, size_t* off, int64_t* count) {
   return MPC_OK;
 }
 
+// the mixed RIGHT events sorted by (gap, read): the multi-workgroup chain when
+// the plan has many reads (it falls back to K_rsort by itself), else K_rsort
+static void launch_rsort(const mpc_plan* p, const Dev& d, hipStream_t st) {
+  const int32_t nrb = (int32_t)((p->N + kRS - 1) / kRS);
+  if (p->rsort_multi) {
+    const int32_t ns = (int32_t)((p->G + 1 + kScanBlk - 1) / kScanBlk);
+    hipLaunchKernelGGL(K_rscan1, dim3(ns), dim3(1024), 0, st, d);
+    hipLaunchKernelGGL(K_rscan2, dim3(ns), dim3(1024), 0, st, d, ns);
+    hipLaunchKernelGGL(K_rscatter, dim3(nrb), dim3(kRS), 0, st, d);
+    hipLaunchKernelGGL(K_rsegsort, dim3((unsigned)((p->G + 1 + 3) / 4)), dim3(256), 0, st, d);
+  }
+  hipLaunchKernelGGL(K_rsort, dim3(1), dim3(kRS), 0, st, d, nrb, (int32_t)p->end_bit);
+}
+
 #define NEED_BOUND(p) do { if (!(p) || !(p)->bound) return fail(MPC_E_STATE, "plan not bound"); } while (0)
 
 int mpc_parse(mpc_plan* p, void* stream) {
@@ -3525,6 +3674,7 @@ int mpc_parse(mpc_plan* p, void* stream) {
     add(d.diff, p->G, 0u);
     add(d.sub, 4 * p->G, 0u);
     add(d.maxR, p->G, 0u);
+    if (p->rsort_multi) add(d.gcnt, p->G + 1, 0u);
     if (p->tally_mode == 4) add(at<int32_t>(p, mpc_plan::B_BKCUR), (int64_t)p->n_parse_wg * p->nbmax, 0u);
     add(d.maxdepth, p->S, 0u);
     add(d.ksum, 2 * p->cnt[mpc_plan::B_KSUM], 0u);  // look-back status words (epoch-tagged as well)
@@ -3557,7 +3707,7 @@ int mpc_index(mpc_plan* p, void* stream) {
   // (one stream: a second one's event fork/join cost more than the overlap, measured)
   const int32_t nub = (int32_t)((p->n_bc + kUnitEntriesPerBlock - 1) / kUnitEntriesPerBlock);  // unit-cutting blocks
   if (nrb + nub > 0) hipLaunchKernelGGL(K_rsplit_units, dim3(nrb + nub), dim3(kRS), 0, st, d, unit_args(p, d), nrb);
-  hipLaunchKernelGGL(K_rsort, dim3(1), dim3(kRS), 0, st, d, nrb, (int32_t)p->end_bit);
+  launch_rsort(p, d, st);
   hipLaunchKernelGGL(K_rstart, dim3(nblk(std::max<int64_t>(p->G + 1, p->N))), dim3(256), 0, st, d);  // (M <= N)
   HIPCHK(hipGetLastError());
   return MPC_OK;
@@ -3640,7 +3790,7 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
       launch_flank(p, d, st);
       break;
     case MPC_K_RSORT:
-      hipLaunchKernelGGL(K_rsort, dim3(1), dim3(kRS), 0, st, d, (int32_t)((p->N + kRS - 1) / kRS), (int32_t)p->end_bit);
+      launch_rsort(p, d, st);
       break;
     default:
       return fail(MPC_E_ARG, "unknown kernel");

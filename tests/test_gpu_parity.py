@@ -346,3 +346,21 @@ def test_mixed_right_sort_paths(pkg, spec, lo, hi):
     m = int(runner.plan.status()[pkg.engine.MPC_ST_MIXED])
     assert lo <= m <= hi, m
     _cmp(runner.fetch()[0], _oracle(samples[0], -1.0, 1.0), ("rsort", m))
+
+
+@pytest.mark.parametrize("spec,lo,hi", [
+    # more than 512 K_rsplit blocks: the multi-workgroup sort (K_rscan, K_rscatter,
+    # K_rsegsort) -- gaps of up to 64 events -- and its fallback to K_rsort
+    # (a gap with more)
+    (dict(n=2000, n_reads=600_000, profile="default", seed=8, frac_partial=0.05), 8193, 600_000),
+    (dict(n=500, n_reads=600_000, profile="indel", seed=9, frac_partial=0.3), 8193, 600_000),
+], ids=["multi", "multi_fallback"])
+def test_mixed_right_sort_many_reads(pkg, spec, lo, hi):
+    syn = pkg.synth.Synth(antisense=False, **spec)
+    samples = [syn.sample(0)]
+    runner = pkg.engine.Runner(samples)
+    runner.step(-1.0, 1.0)
+    runner.check()
+    m = int(runner.plan.status()[pkg.engine.MPC_ST_MIXED])
+    assert lo <= m <= hi, m
+    _cmp(runner.fetch()[0], _oracle(samples[0], -1.0, 1.0), ("rsort many", m))

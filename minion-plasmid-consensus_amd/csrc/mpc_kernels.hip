@@ -2280,12 +2280,20 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       }
     }
     __syncthreads();
+#ifdef MPC_ABL_LEFT_NOFLUSH  // timing ablation only (wrong results): no unit flush
+    for (int q = threadIdx.x; q < 0; q += blockDim.x) {
+#else
     for (int q = threadIdx.x; q < kBW * kKMax; q += blockDim.x) {
+#endif
       const int k = q % kKMax, p = q / kKMax;
       const uint32_t m = Ml[p * kMs + k];
       if (m) atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + k, (int32_t)m);
     }
+#ifdef MPC_ABL_LEFT_NOFLUSH
+    for (int q = threadIdx.x; q < 0; q += blockDim.x) {
+#else
     for (int q = threadIdx.x; q < kBW * kKMax * 16; q += blockDim.x) {  // contiguous per (gap, run)
+#endif
       const int k = (q >> 4) % kKMax, p = (q >> 4) / kKMax;
       const uint32_t v = Tl[p * kTs + k * 16 + (q & 15)];
       if (v) atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + k) * 16 + (q & 15), v);
@@ -2305,7 +2313,11 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     atomicMax(a.M + run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + o.read), o.len);
   }
   // upstream flanks (block-uniform trips: block_atomic_max synchronizes the block)
+#ifdef MPC_ABL_LEFT_NOREADS  // timing ablation only (wrong results): no per-read pass
+  for (int64_t r0 = fb * blockDim.x; r0 < 0; r0 += nthreads) {
+#else
   for (int64_t r0 = fb * blockDim.x; r0 < a.N; r0 += nthreads) {
+#endif
     const int64_t r = r0 + threadIdx.x;
     int64_t run = 0;
     int32_t L = 0;

@@ -2568,7 +2568,14 @@ __device__ __forceinline__ int code_exact(uint32_t c) {
   return c == expect ? code : -1;
 }
 
-constexpr int kStageB = 16384;  // flank bytes staged in LDS per chunk (a block's range is processed in chunks; C2: 1 per side)
+constexpr int kStageB = 16384;
+// K_flank per-byte loop: 4 consecutive bytes per thread (1) or one (0)
+#ifndef MPC_FLANK_BYTES4
+#define MPC_FLANK_BYTES4 0
+#endif
+#ifndef MPC_FLANK_BLOCKS_MAX
+#define MPC_FLANK_BLOCKS_MAX 1024
+#endif  // flank bytes staged in LDS per chunk (a block's range is processed in chunks; C2: 1 per side)
 
 // Byte-parallel: the block's flank bytes (both sides) are staged in LDS chunk by
 // chunk; every thread takes 4 consecutive bytes.  The owner of a byte is found
@@ -2718,6 +2725,7 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
         }
       }
       __syncthreads();
+#if MPC_FLANK_BYTES4
       // every thread takes 4 consecutive bytes (one owner lookup, one stage
       // dword); consecutive lanes, consecutive dwords: a flank's bytes go to
       // consecutive rows, so a wave's (rare) global atomics cover a few
@@ -2754,6 +2762,32 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
       }
     }
   }
+#else
+      // consecutive lanes take consecutive bytes: a flank's bytes go to
+      // consecutive rows, so a wave's (rare) global atomics cover a few
+      // contiguous segments instead of one scattered row per lane
+      // 32-bit: rows < row_cap < 2^31, a block's flank bytes < 2^31
+      const int cn32 = (int)cn, c032 = (int)c0;
+      const int32_t w032 = w0 >= 0 ? (int32_t)w0 : -(1 << 30);  // no window: never a hit
+#ifdef MPC_ABL_FLANK_NOBYTES  // timing ablation only (wrong results): no per-byte tallies
+      for (int x = tid; x < 0; x += blockDim.x) {
+#else
+      for (int x = tid; x < cn32; x += blockDim.x) {
+#endif
+        const uint32_t word = bm[x >> 5];
+        const int o = wpre[x >> 5] + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
+        const int32_t rw = t_row[o];
+        if (rw < 0) continue;
+        const int32_t row = rw + (c032 + x - t_start[o]);
+        const int code = code_exact(stage[x + sh0]);
+        if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
+        const uint32_t wr = (uint32_t)(row - w032);
+        if (wr < (uint32_t)kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
+        else atomicAdd(a.rows + (int64_t)row * 4 + code, 1u);
+      }
+    }
+  }
+#endif
   }  // chunks
   __syncthreads();
   for (int side = 0; side < 2; ++side) {
@@ -3162,7 +3196,7 @@ static int64_t ins_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::mi
 static int flank_reads(const mpc_plan* p) { return (p->N + kFR - 1) / kFR < 256 ? kFRSmall : kFR; }
 // K_flank blocks: chunks of flank_reads reads, at most about four resident
 // blocks per CU (each further chunk of a block shares its window flush)
-constexpr int64_t kFlankBlocksMax = 1024;
+constexpr int64_t kFlankBlocksMax = MPC_FLANK_BLOCKS_MAX;
 static int64_t flank_grid(const mpc_plan* p) {
   const int fr = flank_reads(p);
   return std::max<int64_t>(1, std::min<int64_t>(kFlankBlocksMax, (p->N + fr - 1) / fr));

@@ -2574,7 +2574,7 @@ constexpr int kStageB = 16384;
 #define MPC_FLANK_BYTES4 0
 #endif
 #ifndef MPC_FLANK_BLOCKS_MAX
-#define MPC_FLANK_BLOCKS_MAX 1024
+#define MPC_FLANK_BLOCKS_MAX (1 << 30)
 #endif  // flank bytes staged in LDS per chunk (a block's range is processed in chunks; C2: 1 per side)
 
 // Byte-parallel: the block's flank bytes (both sides) are staged in LDS chunk by

@@ -1,12 +1,7 @@
 #!/bin/bash
 set -o pipefail
 # The round's final measurements part 1 (scripts/final_r04a.sh: smoke, suite,
-# bench line + its kernel stats, PMC traffic), then the K_flank grid / loop
-# shape at C3 and the LDS counters of K_left
+# bench line + its kernel stats, PMC traffic)
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out; cd $R
-bash scripts/final_r04a.sh || exit 1
-for v in fl_b1_g1024 fl_b4_g1024; do
-  bash scripts/kstats_full_variant.sh km_${v}_c3 c3 exp/v/$v.so 40 | grep -E "==|K_flank" || exit 1
-done
-bash scripts/pmc_full_variant.sh pm_left_c3 c3 exp/v/fl_b1_ginf.so K_left || exit 1
+bash scripts/final_r04a.sh

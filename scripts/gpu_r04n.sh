@@ -7,3 +7,7 @@ for v in fl_b1_g1024 fl_b4_g1024; do
   bash scripts/kstats_full_variant.sh km_${v}_c3 c3 exp/v/$v.so 40 | grep -E "==|K_flank" || exit 1
 done
 bash scripts/pmc_full_variant.sh pm_left_c3 c3 exp/v/fl_b1_ginf.so K_left || exit 1
+timeout -k 10 200 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 \
+  exp/dist_overhead.py c2 2>&1 | grep -v "^\[W\|Warning" | tee gpurun_out/dist_overhead.txt || exit 1
+timeout -k 10 200 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29542 \
+  exp/dist_graph.py c2 2>&1 | grep -v "^\[W\|Warning" | tee gpurun_out/dist_graph.txt

@@ -251,6 +251,8 @@ def main():
                     help="CUs the parse grid is sized for with batches in flight (default: per config)")
     ap.add_argument("--dist", action="store_true",
                     help="take the distributed path (process group + dist.DistExchange) even at WORLD_SIZE=1")
+    ap.add_argument("--graph", action="store_true",
+                    help="distributed path: replay every pipeline's step from a HIP graph (no host dispatch)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--hbm-config", default="c3",
@@ -330,6 +332,41 @@ def main():
     torch.cuda.synchronize()
     for r in runners:
         r.check()  # data-error flags must be clear (valid synthetic input)
+
+    # --graph (distributed path): every pipeline's step -- phase launches, torch
+    # glue ops and RCCL collectives -- captured once in a HIP graph and replayed,
+    # so a step costs no host dispatch (exp/dist_graph.py).  All ranks capture
+    # the same sequence; if any rank fails to, every rank stays eager.
+    graph_note = None
+    if args.graph and use_dist and cfg != "c5":
+        graphs, ok = [], 1
+        try:
+            for r in runners:
+                g = torch.cuda.CUDAGraph()
+                cap = torch.cuda.Stream()
+                with torch.cuda.stream(cap):
+                    r.step(mdf, gtf)
+                    cap.synchronize()
+                    with torch.cuda.graph(g, stream=cap):
+                        r.step(mdf, gtf)
+                graphs.append(g)
+            torch.cuda.synchronize()
+        except Exception as e:  # noqa: BLE001 (any capture failure: eager)
+            ok, graph_note = 0, "capture failed: %s" % str(e)[:200]
+        t = torch.tensor([ok], dtype=torch.int64, device=coll_dev)
+        dist.all_reduce(t, op=dist.ReduceOp.MIN)
+        if int(t.item()) == 1:
+            def step(k):  # noqa: F811 (replaces the eager step)
+                with torch.cuda.stream(streams[k % R]):
+                    graphs[k % R].replay()
+            for k in range(R):
+                step(k)
+            torch.cuda.synchronize()
+            for r in runners:
+                r.check()
+            graph_note = "steps replayed from HIP graphs (one per pipeline)"
+        elif graph_note is None:
+            graph_note = "another rank failed to capture: eager steps"
 
     def barrier():
         if use_dist:
@@ -456,7 +493,7 @@ def main():
                        "min_depth_factor": mdf, "global_threshold_factor": gtf,
                        "parallelism": ("replicas" if cfg == "c5" else "read-shard") + f"x{world}",
                        "batches_in_flight": R, "parse_cus": cus or 256,
-                       "process_group": backend if use_dist else None},
+                       "process_group": backend if use_dist else None, "graph": graph_note},
             "single_batch_ms_per_step": single_ms,
             "what": ("value = aligned bases of K steps / wall time with %d batch copies in flight on %d streams "
                      "(pipelined throughput); single_batch_ms_per_step = the same config one batch at a time" % (R, R)

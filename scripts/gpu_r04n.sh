@@ -11,3 +11,6 @@ timeout -k 10 200 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node
   exp/dist_overhead.py c2 2>&1 | grep -v "^\[W\|Warning" | tee gpurun_out/dist_overhead.txt || exit 1
 timeout -k 10 200 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29542 \
   exp/dist_graph.py c2 2>&1 | grep -v "^\[W\|Warning" | tee gpurun_out/dist_graph.txt
+timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29543 \
+  bench.py --dist --graph --steps 20 --warmup 3 --no-cpu-baseline --no-e2e --hbm-config '' > gpurun_out/bdg.log 2>&1 || { tail -20 gpurun_out/bdg.log; exit 1; }
+grep '^{' gpurun_out/bdg.log | tail -1 | cut -c1-200; grep -o '"graph": "[^"]*"' gpurun_out/bdg.log

@@ -333,10 +333,13 @@ def main():
     for r in runners:
         r.check()  # data-error flags must be clear (valid synthetic input)
 
-    # --graph (distributed path): every pipeline's step -- phase launches, torch
-    # glue ops and RCCL collectives -- captured once in a HIP graph and replayed,
-    # so a step costs no host dispatch (exp/dist_graph.py).  All ranks capture
-    # the same sequence; if any rank fails to, every rank stays eager.
+    # distributed path: every pipeline's step -- phase launches, torch glue ops
+    # and RCCL collectives -- captured once in a HIP graph and replayed, so a
+    # step costs no host dispatch (world size 1 over RCCL, C2: eager 220 us /
+    # step with 141 us of host dispatch, replay 202.5 us = the local runner;
+    # profiles/r04_experiments/dist_graph_world1.txt).  All ranks capture the
+    # same sequence; if any rank fails to, every rank stays eager.  Opt-in: the
+    # capture of RCCL collectives has run at world size 1 only (one GPU here).
     graph_note = None
     if args.graph and use_dist and cfg != "c5":
         graphs, ok = [], 1

@@ -3,7 +3,7 @@ set -o pipefail
 # K_flank grid / loop shape at C3 and the LDS counters of K_left
 R=${GRAFT_REPO_ROOT:-$(pwd)}
 mkdir -p $R/gpurun_out; cd $R
-for v in fl_b1_g1024 fl_b4_g1024; do
+for v in fl_b1_ginf fl_b1_g1024 fl_b4_g1024; do
   bash scripts/kstats_full_variant.sh km_${v}_c3 c3 exp/v/$v.so 40 | grep -E "==|K_flank" || exit 1
 done
 bash scripts/pmc_full_variant.sh pm_left_c3 c3 exp/v/fl_b1_ginf.so K_left || exit 1

@@ -14,3 +14,5 @@ timeout -k 10 200 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node
 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29543 \
   bench.py --dist --graph --steps 20 --warmup 3 --no-cpu-baseline --no-e2e --hbm-config '' > gpurun_out/bdg.log 2>&1 || { tail -20 gpurun_out/bdg.log; exit 1; }
 grep '^{' gpurun_out/bdg.log | tail -1 | cut -c1-200; grep -o '"graph": "[^"]*"' gpurun_out/bdg.log
+bash scripts/pmc_traffic.sh f4pmc c2 c3 || exit 1
+cat gpurun_out/pmc_traffic_c2.json gpurun_out/pmc_traffic_c3.json

@@ -9,8 +9,6 @@ done
 bash scripts/pmc_full_variant.sh pm_left_c3 c3 exp/v/fl_b1_ginf.so K_left || exit 1
 timeout -k 10 200 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29541 \
   exp/dist_overhead.py c2 2>&1 | grep -v "^\[W\|Warning" | tee gpurun_out/dist_overhead.txt || exit 1
-timeout -k 10 200 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29542 \
-  exp/dist_graph.py c2 2>&1 | grep -v "^\[W\|Warning" | tee gpurun_out/dist_graph.txt
 timeout -k 10 300 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 1 --master-addr 127.0.0.1 --master-port 29543 \
   bench.py --dist --graph --steps 20 --warmup 3 --no-cpu-baseline --no-e2e --hbm-config '' > gpurun_out/bdg.log 2>&1 || { tail -20 gpurun_out/bdg.log; exit 1; }
 grep '^{' gpurun_out/bdg.log | tail -1 | cut -c1-200; grep -o '"graph": "[^"]*"' gpurun_out/bdg.log

@@ -364,3 +364,25 @@ def test_mixed_right_sort_many_reads(pkg, spec, lo, hi):
     m = int(runner.plan.status()[pkg.engine.MPC_ST_MIXED])
     assert lo <= m <= hi, m
     _cmp(runner.fetch()[0], _oracle(samples[0], -1.0, 1.0), ("rsort many", m))
+
+
+def test_mode3_windows_with_an_empty_sample(pkg):
+    """Tally mode 3 with two substitution windows per sample (K_subs slab rows
+    summed by K_subsum per sample and window) and a sample without reads in
+    the same launch (no K_subs blocks, no K_subsum work: its tallies stay the
+    cleared zeros)."""
+    n = geo.first_length(3, 16384 + 100)
+    syn = pkg.synth.Synth(n=n, n_reads=300, profile="indel", seed=71, frac_partial=0.3, antisense=False)
+    full = syn.sample(0)
+    empty = dict(full)
+    empty.update(cs=np.zeros(0, np.uint8), cs_off=np.zeros(1, np.int64), tstart=np.zeros(0, np.int64),
+                 up=np.zeros(0, np.uint8), up_off=np.zeros(1, np.int64), down=np.zeros(0, np.uint8),
+                 down_off=np.zeros(1, np.int64), aligned=np.zeros(0, np.int64))
+    samples = [full, empty, full]
+    runner = pkg.engine.Runner(samples)
+    assert runner.plan.info()["tally_mode"] == 3
+    for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
+        runner.step(mdf, gtf)
+        runner.check()
+        for k, (got, smp) in enumerate(zip(runner.fetch(), samples)):
+            _cmp(got, _oracle(smp, mdf, gtf), ("mode3 empty", k, mdf))

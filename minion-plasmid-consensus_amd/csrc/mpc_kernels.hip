@@ -851,6 +851,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int64_t sev_base = (P - a.cs_base) / 3 + 2 * ra;  // ... and its substitution-event regions (TM 3)
   uint32_t nsub_v = 0;                                    // lane k: substitution events of window k
   uint32_t nev = 0;                                       // events written (wave-uniform)
+#ifdef MPC_ABL_TOKENIZE_ONLY
+  uint32_t nunit = 0;  // timing ablation: decoded units written (pass-1 cost of a split parse)
+#endif
   int64_t rs0 = ra;         // first read whose cs starts at or after P
   bool carry = false;       // slot 0 holds a read continuing into this window
   int32_t c_base = 0;       // ... and its coordinate base (wave-uniform): i = base + window prefix of advances
@@ -1183,6 +1186,13 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       }
 #endif
       MPC_SEG(2);
+#ifdef MPC_ABL_TOKENIZE_ONLY  // timing ablation only (wrong results): decode, one packed word per unit, no effects
+      if (v) a.ins_raw[ev_base + nunit + l] = (uint64_t)(uint32_t)(adv0 + adv) | ((uint64_t)kind << 32) |
+                                              ((uint64_t)pay << 40) | ((uint64_t)(olen_e & 0xffff) << 48) | (uint64_t)err;
+      nunit += (uint32_t)__popcll(ballot(v));
+      qc += __popcll(brs);
+      continue;
+#endif
       // ---- coordinates ----
       const int advu = adv0 + adv;            // unit advance <= 2^23: 64 lanes stay < 2^29
       const int ainc = wave_scan_i32(advu);

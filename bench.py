@@ -184,9 +184,10 @@ def e2e_cli(pkg, cfg, reps=2):
 
 
 # what bounds K_parse by its counters (profiles/r03_stalls_*)
-LIMITER = ("dependency latency of the per-round chain (three dependent LDS round trips and a DPP scan per 64 "
-           "units): waves issue 36 %, wait on s_waitcnt 35 %, dependency-stalled 29 % of their cycles; VALU at "
-           "35-60 % of its measured 4-wave rate (profiles/r03_stalls_c2_final, profiles/r03_micro; DESIGN.md §3)")
+LIMITER = ("dependency latency of the per-round chain (dependent LDS round trips and a DPP scan per 64 units): "
+           "waves issue 36 %, wait on s_waitcnt 35 %, dependency-stalled 29 % of their cycles; VALU at 35-60 % of "
+           "its measured 4-wave rate (profiles/r03_stalls_c2_final, profiles/r03_micro); window + decode work "
+           "(no effects) is 65-71 % of the kernel (profiles/r04_experiments/kparse_tokenize_only.txt; DESIGN.md §3)")
 
 
 # roofline.bound: what limits K_parse as measured (its HBM fraction is still

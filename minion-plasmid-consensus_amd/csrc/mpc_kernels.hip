@@ -238,7 +238,9 @@ __device__ __forceinline__ int64_t readlane64(int64_t x, int j) {
 // stamps around K_parse's segments, summed per wave in scalar registers and
 // stored once per wave into g_stamps (nothing else reads them).  The product
 // build compiles none of this.
-#ifdef MPC_STAMPS
+// -DMPC_STAMPS_LEFT: the same stamps around K_left's segments instead
+// (scripts/kleft_stamps.py).
+#if defined(MPC_STAMPS) || defined(MPC_STAMPS_LEFT)
 constexpr int kStampSeg = 8, kStampWaves = 1 << 16;
 __device__ uint64_t g_stamps[kStampWaves * kStampSeg];
 #define MPC_STAMP(t)                                                                   \
@@ -247,15 +249,23 @@ __device__ uint64_t g_stamps[kStampWaves * kStampSeg];
     asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");        \
     __builtin_amdgcn_sched_barrier(0);                                               \
   } while (0)
-#define MPC_SEG(k)                  \
+#define MPC_SEG_ALWAYS(k)           \
   do {                              \
     uint64_t t_;                    \
     MPC_STAMP(t_);                  \
     st_acc[k] += t_ - st_prev;      \
     st_prev = t_;                   \
   } while (0)
+#endif
+#ifdef MPC_STAMPS
+#define MPC_SEG(k) MPC_SEG_ALWAYS(k)
 #else
 #define MPC_SEG(k) do {} while (0)
+#endif
+#ifdef MPC_STAMPS_LEFT
+#define MPC_LSEG(k) MPC_SEG_ALWAYS(k)
+#else
+#define MPC_LSEG(k) do {} while (0)
 #endif
 
 // ---------------------------------------------------------------------------
@@ -2215,13 +2225,19 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
   constexpr int kLV = UB == 512 ? 3072 : kLeftVals;
   __shared__ int32_t s_vals[kLV];         // the bucket's mixed RIGHT reads (vals_out), searched per event
   // (K_units raises DE_INTERNAL instead of overrunning the unit list)
+#ifdef MPC_STAMPS_LEFT
+  uint64_t st_acc[kStampSeg] = {0, 0, 0, 0, 0, 0, 0, 0}, st_prev;
+  MPC_STAMP(st_prev);
+#endif
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
     for (int k = threadIdx.x; k < kBW * kMs; k += blockDim.x) Ml[k] = 0;
     for (int k = threadIdx.x; k < kBW * kTs; k += blockDim.x) Tl[k] = 0;
+    MPC_LSEG(0);
     const UnitView uv = load_unit<false>(a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, a.right_start, a.rsl,
                                          a.roff, nullptr, nullptr, nullptr, a.pwork, s_r0, s_pre, s_src, s_wsum, s_rs,
                                          s_rsl, s_roff, nullptr);
+    MPC_LSEG(1);
     const int n = uv.n;
     const int gb = uv.gb;
     const int g0 = uv.g0;
@@ -2250,7 +2266,9 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     const int32_t v0 = s_rsl[0], vn = s_rsl[uv.gl + 1 - g0] - v0;
     const bool vl = vn <= kLV;
     for (int k = threadIdx.x; vl && k < vn; k += blockDim.x) s_vals[k] = a.vals_out[v0 + k];
+    MPC_LSEG(2);
     __syncthreads();
+    MPC_LSEG(3);
 #pragma unroll
     for (int q = 0; q < kEPT; ++q) {
       const uint32_t ev = evs[q];
@@ -2289,7 +2307,9 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
         for (int j = 0; j < L; ++j) atomicAdd(rt + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
       }
     }
+    MPC_LSEG(4);
     __syncthreads();
+    MPC_LSEG(5);
 #ifdef MPC_ABL_LEFT_NOFLUSH  // timing ablation only (wrong results): no unit flush
     for (int q = threadIdx.x; q < 0; q += blockDim.x) {
 #else
@@ -2309,6 +2329,7 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       if (v) atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + k) * 16 + (q & 15), v);
     }
     __syncthreads();
+    MPC_LSEG(6);
   }
   const int64_t nthreads = (int64_t)gridDim.x * blockDim.x;
   // the per-read parts start at the first block that had no unit (rotated
@@ -2347,6 +2368,16 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     }
     block_atomic_max(a.M, run, L, ok, &s_key, &s_val);
   }
+#ifdef MPC_STAMPS_LEFT
+  MPC_LSEG(7);
+  const int64_t gw = (int64_t)blockIdx.x * (UB / 64) + (threadIdx.x >> 6);
+  if (lane() < kStampSeg && gw < kStampWaves) {
+    uint64_t v = 0;
+#pragma unroll
+    for (int k = 0; k < kStampSeg; ++k) v = lane() == k ? st_acc[k] : v;
+    g_stamps[gw * kStampSeg + lane()] = v;
+  }
+#endif
 }
 
 // ---------------------------------------------------------------------------
@@ -3855,8 +3886,8 @@ int mpc_profile_kernel(mpc_plan* p, int which, void* stream) {
   return MPC_OK;
 }
 
-#ifdef MPC_STAMPS
-// diagnostic build only: per-wave K_parse segment cycle sums (kStampSeg per wave)
+#if defined(MPC_STAMPS) || defined(MPC_STAMPS_LEFT)
+// diagnostic build only: per-wave K_parse (K_left) segment cycle sums (kStampSeg per wave)
 int mpc_debug_stamps(uint64_t* out, int64_t n_words) {
   const int64_t nw = std::min<int64_t>(n_words, (int64_t)kStampWaves * kStampSeg);
   HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(g_stamps), (size_t)nw * 8, 0, hipMemcpyDeviceToHost));

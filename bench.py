@@ -17,7 +17,7 @@ exactly those reads of the full set) and the ranks exchange the small per-gap
   c3           strong scaling: 1M reads in total, N slices (BASELINE configs[2])
   c5           sample-partitioned replicas: 12 plasmids per GPU, no collective
 
-Batches in flight (--inflight R, default 2): R independent pipelines (each its
+Batches in flight (--inflight R, default 3 at C2, else 2): R independent pipelines (each its
 own device copy of the batch and its own workspace) on R streams, taken in
 turn, so one batch's latency-bound post-parse chain overlaps the next batch's
 parse -- a stream of plasmid batches as a sequencing run produces them.  Every
@@ -74,8 +74,12 @@ CONFIGS = {
            "(96 over 8 GPUs), sense+antisense, sample-partitioned"),
 }
 C5_PER_GPU = 12
-# CUs the parse grid is sized for when batches are in flight (bench --inflight >= 2)
-PARSE_CUS_INFLIGHT = {"c1": 128, "c2": 160, "c3": 224, "c4": 224, "c5": 192}
+# batches in flight per config, and the CUs the parse grid is sized for with
+# them: C2 3 / 192 (20-step runs: 2 / 160 200 us per step, 3 / 192 182.5 us,
+# 4 / 128 183 us; profiles/r04_experiments/c2_batches_in_flight.txt), the
+# others 2 (profiles/r03_experiments/parse_cus_inflight.txt)
+INFLIGHT = {"c1": 2, "c2": 3, "c3": 2, "c4": 2, "c5": 2}
+PARSE_CUS_INFLIGHT = {"c1": 128, "c2": 192, "c3": 224, "c4": 224, "c5": 192}
 PORT_SAMPLE_BASES = 2_500_000_000  # bound of the live CPU-port timing (~6 s of C at ~4e8 b/s)
 E2E_CONFIGS = ("c1", "c2", "c3", "c4", "c5")
 
@@ -246,8 +250,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--kernel-reps", type=int, default=20)
-    ap.add_argument("--inflight", type=int, default=2,
-                    help="batches in flight (independent pipelines on their own streams, taken in turn)")
+    ap.add_argument("--inflight", type=int, default=None,
+                    help="batches in flight (independent pipelines on their own streams, taken in turn; "
+                         "default per config: INFLIGHT)")
     ap.add_argument("--parse-cus", type=int, default=None,
                     help="CUs the parse grid is sized for with batches in flight (default: per config)")
     ap.add_argument("--dist", action="store_true",
@@ -292,10 +297,10 @@ def main():
     # post-parse chain overlaps the next batch's parse (a stream of plasmid
     # batches, as a sequencing run produces; every step is still one full pass
     # over one batch)
-    R = max(1, args.inflight)
+    R = max(1, args.inflight if args.inflight is not None else INFLIGHT[cfg])
     # with batches in flight the parse grid is sized for fewer CUs, so the other
     # batch's post-parse kernels (which cannot share a CU with the parse: it holds
-    # every VGPR) run beside it; measured per config with 2 in flight
+    # every VGPR) run beside it; measured per config at its default R
     # (profiles/r03_experiments/parse_cus_inflight.txt, c1_parse_workgroups_inflight.txt);
     # every rank of an N-GPU run does the same (weak scaling: the same per-GPU batch)
     cus = (args.parse_cus if args.parse_cus is not None else PARSE_CUS_INFLIGHT[cfg]) if R > 1 else 0
@@ -405,12 +410,13 @@ def main():
         return float(np.mean([a.elapsed_time(b) for a, b in ev]))
 
     # K_parse on the plan that was TIMED: with batches in flight its grid is
-    # sized for `cus` CUs and the other batch's step runs beside it
+    # sized for `cus` CUs and the other batches' steps run beside it
     timed_k_ms = None
     if R > 1:
-        def other():
-            with torch.cuda.stream(streams[1]):
-                runners[1].step(mdf, gtf)
+        def other():  # the other pipelines' steps, as in the timed loop
+            for k in range(1, R):
+                with torch.cuda.stream(streams[k]):
+                    runners[k].step(mdf, gtf)
         timed_k_ms = kparse_ms(runners[0].plan, args.kernel_reps, streams[0], other)
         timed_geo = runners[0].plan.info()
         for k in range(R):
@@ -511,8 +517,8 @@ def main():
                 "bound": ROOF_BOUND, "kernel": "K_parse", "achieved": alg_bytes / (timed_k_ms * 1e-3) / 1e9,
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": alg_bytes / (timed_k_ms * 1e-3) / 1e9 / HBM_PEAK_GBS,
                 "mean_launch_us": timed_k_ms * 1e3, "parse_workgroups": timed_geo["parse_workgroups"],
-                "plan": "the timed plan: parse grid sized for %d CUs, the other batch's step on its own stream "
-                        "beside every launch" % cus},
+                "plan": "the timed plan: parse grid sized for %d CUs, the other %d batches' steps on their own "
+                        "streams beside every launch" % (cus, R - 1)},
             "roofline_hbm": hbm,
             "cpu_baseline": cpu,
             "e2e": e2e,

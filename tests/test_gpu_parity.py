@@ -161,22 +161,22 @@ def test_repeat_launches_identical(pkg):
             _cmp(got, first, "repeat")
 
 
-@pytest.mark.parametrize("parse_cus", [0, 40])
-def test_batches_in_flight_on_two_streams(pkg, parse_cus):
-    """bench.py --inflight: independent plans on two streams, steps interleaved
+@pytest.mark.parametrize("parse_cus,R", [(0, 2), (40, 2), (48, 3)])
+def test_batches_in_flight_on_two_streams(pkg, parse_cus, R):
+    """bench.py --inflight: independent plans on R streams, steps interleaved
     without host synchronisation, each equal to the oracle (the look-back status
     words of concurrent launches carry different epochs); with the parse grid
     sized for fewer CUs (mpc_input.parse_cus) as bench.py does."""
     import torch
     syn = pkg.synth.Synth(n=2686, n_reads=6000, profile="default", seed=91, frac_partial=0.2)
     samples = [syn.sample(0), syn.sample(1)]
-    runners = [pkg.engine.Runner(samples, parse_cus=parse_cus) for _ in range(2)]
+    runners = [pkg.engine.Runner(samples, parse_cus=parse_cus) for _ in range(R)]
     if parse_cus:
         assert runners[0].plan.info()["parse_workgroups"] <= parse_cus
-    streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
-    for k in range(8):
-        with torch.cuda.stream(streams[k % 2]):
-            runners[k % 2].step(0.1, 5.0)
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in range(R - 1)]
+    for k in range(4 * R):
+        with torch.cuda.stream(streams[k % R]):
+            runners[k % R].step(0.1, 5.0)
     torch.cuda.synchronize()
     exp = [_oracle(s, 0.1, 5.0) for s in samples]
     for r in runners:

@@ -17,7 +17,7 @@ exactly those reads of the full set) and the ranks exchange the small per-gap
   c3           strong scaling: 1M reads in total, N slices (BASELINE configs[2])
   c5           sample-partitioned replicas: 12 plasmids per GPU, no collective
 
-Batches in flight (--inflight R, default 3 at C2, else 2): R independent pipelines (each its
+Batches in flight (--inflight R, default per config: C1 4, C2 3, else 2): R independent pipelines (each its
 own device copy of the batch and its own workspace) on R streams, taken in
 turn, so one batch's latency-bound post-parse chain overlaps the next batch's
 parse -- a stream of plasmid batches as a sequencing run produces them.  Every
@@ -75,11 +75,13 @@ CONFIGS = {
 }
 C5_PER_GPU = 12
 # batches in flight per config, and the CUs the parse grid is sized for with
-# them: C2 3 / 192 (20-step runs: 2 / 160 200 us per step, 3 / 192 182.5 us,
-# 4 / 128 183 us; profiles/r04_experiments/c2_batches_in_flight.txt), the
-# others 2 (profiles/r03_experiments/parse_cus_inflight.txt)
-INFLIGHT = {"c1": 2, "c2": 3, "c3": 2, "c4": 2, "c5": 2}
-PARSE_CUS_INFLIGHT = {"c1": 128, "c2": 192, "c3": 224, "c4": 224, "c5": 192}
+# them (20-step runs): C2 3 / 192 (2 / 160 200 us per step, 3 / 192 182.5 us,
+# 4 / 128 183 us; profiles/r04_experiments/c2_batches_in_flight.txt), C1
+# 4 / 96 (2 / 128 85 us, 3 / 128 69 us, 4 / 96 62 us), C3-C5 2 (3 is no
+# faster: batches_in_flight_c1_c3_c4_c5.txt; their CUs:
+# profiles/r03_experiments/parse_cus_inflight.txt)
+INFLIGHT = {"c1": 4, "c2": 3, "c3": 2, "c4": 2, "c5": 2}
+PARSE_CUS_INFLIGHT = {"c1": 96, "c2": 192, "c3": 224, "c4": 224, "c5": 192}
 PORT_SAMPLE_BASES = 2_500_000_000  # bound of the live CPU-port timing (~6 s of C at ~4e8 b/s)
 E2E_CONFIGS = ("c1", "c2", "c3", "c4", "c5")
 

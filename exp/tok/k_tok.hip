@@ -90,6 +90,30 @@ __device__ __forceinline__ uint32_t op_fields(uint64_t v, int64_t s, int64_t e) 
   return (uint32_t)(ol > 63 ? 63 : ol) << 4 | pay << 10;
 }
 
+// special byte by one 64-bit mask lookup (':' '+' '-' '*' < 64) or 'Z'
+__device__ __forceinline__ bool special_lut(uint32_t c) {
+  constexpr uint64_t kSp = (1ull << ':') | (1ull << '+') | (1ull << '-') | (1ull << '*');
+  return c < 64 ? (kSp >> c) & 1ull : c == 'Z';
+}
+// ':' operand of nd bytes (v: its first 8) as a number, 16383 = escape: SWAR
+// digit check and three multiply-add folds (pairs, quads, the 8 digits)
+__device__ __forceinline__ uint32_t colon_swar(uint64_t v, int nd) {
+  if (nd < 1 || nd > 8) return 16383u;
+  const uint64_t m = nd == 8 ? ~0ull : (1ull << (8 * nd)) - 1ull;
+  const uint64_t t = v ^ 0x3030303030303030ull;  // digit bytes -> 0..9
+  if ((((t + 0x7676767676767676ull) | t) & 0x8080808080808080ull & m) != 0) return 16383u;
+  uint64_t y = (t & m) << (8 * (8 - nd));  // right-aligned: leading zero digits
+  y = (y * 10 + (y >> 8)) & 0x00FF00FF00FF00FFull;
+  y = (y * 100 + (y >> 16)) & 0x0000FFFF0000FFFFull;
+  y = (y * 10000 + (y >> 32)) & 0xFFFFFFFFull;
+  return y < 16383u ? (uint32_t)y : 16383u;
+}
+__device__ __forceinline__ uint32_t op_fields_swar(uint64_t v, int ol) {
+  const uint32_t p = ((uint32_t)v >> 1) & 0x03030303u;
+  const uint32_t pay = (p | p >> 6 | p >> 12 | p >> 18) & (ol >= 4 ? 0xffu : (1u << (2 * (ol > 0 ? ol : 0))) - 1u);
+  return (uint32_t)(ol > 63 ? 63 : ol) << 4 | pay << 10;
+}
+
 struct TokArgs {
   const uint8_t* cs; int64_t B;
   const int64_t* cs_off; int64_t N;
@@ -199,55 +223,44 @@ __global__ __launch_bounds__(kWaves * 64) void K_tok(TokArgs a) {
       const uint32_t j = j0 + l;
       const bool valid = j < n_own;
       const int s = valid ? list[j] : 0;
-      int64_t e = a.B;  // successor start (absolute)
-      if (j + 1 < n_list) e = A + list[j + 1];
-      else if (valid) {  // rare: no start in the rest of the staged bytes -- scan global memory
-        int64_t p = A + kStaged, rr = rn;
-        while (rr < a.N && a.cs_off[rr] < p) ++rr;
-        const int64_t nr = rr < a.N ? a.cs_off[rr] : INT64_MAX;
-        while (p < a.B && p < nr && !is_special(a.cs[p])) ++p;
-        e = p < a.B ? p : a.B;
-      }
-      const int64_t sa = A + s;
+      const bool has_nx = j + 1 < n_list;
+      const int eq = has_nx ? (int)list[j + 1] : kStaged;  // successor, step offset
       const uint32_t op = by[s];
       const uint32_t rs = (rsb[s >> 5] >> (s & 31)) & 1u;
-      const int64_t eq = e - A;
-      uint32_t nx = 0, rs_e = 0;
-      if (valid && e < a.B) {
-        if (eq < kStaged) { nx = by[eq]; rs_e = (rsb[eq >> 5] >> (eq & 31)) & 1u; }
-        else {
-          nx = a.cs[e];
-          int64_t rr = rn;
-          while (rr < a.N && a.cs_off[rr] < e) ++rr;
-          rs_e = rr < a.N && a.cs_off[rr] == e;
+      uint32_t nx = has_nx ? (uint32_t)by[eq] : 0u;      // zero padding past B: not special
+      uint32_t rs_e = has_nx ? (rsb[eq >> 5] >> (eq & 31)) & 1u : 0u;
+      int len = eq - s - 1;                               // operand bytes
+      if (__ballot(valid && !has_nx)) {  // rare, wave-uniform: no start in the rest of the staged bytes
+        if (valid && !has_nx) {
+          int64_t p = A + kStaged, rr = rn;
+          while (rr < a.N && a.cs_off[rr] < p) ++rr;
+          const int64_t nr = rr < a.N ? a.cs_off[rr] : INT64_MAX;
+          while (p < a.B && p < nr && !is_special(a.cs[p])) ++p;
+          const int64_t e = p < a.B ? p : a.B;
+          const int64_t ol = e - (A + s) - 1;
+          len = ol > 0x3fffffff ? 0x3fffffff : (int)ol;
+          nx = e < a.B ? (uint32_t)a.cs[e] : 0u;
+          rs_e = e < a.B && e == nr;
         }
       }
-      // this token's own ':' value (from the staged bytes: s < 1024, the digits end by s + 9)
-      const uint32_t v_self = op == ':' ? colon_value(load8(reinterpret_cast<const uint8_t*>(by), s + 1), sa, e) : 0u;
+      const uint64_t v = load8(reinterpret_cast<const uint8_t*>(by), s + 1);  // the operand's first 8 bytes
+      const bool colon = op == ':', spc = special_lut(op);
+      const uint32_t v_self = colon ? colon_swar(v, len) : 0u;
       // the previous token: lane l - 1, else the carry
       uint32_t op_p = from_lane_below(op), rs_p = from_lane_below(rs), v_p = from_lane_below(v_self);
       if (l == 0) {
-        if (!c.have_val && c.op == ':') c.val = colon_value(load8(a.cs, c.pos + 1), c.pos, sa);
+        if (!c.have_val && c.op == ':') c.val = colon_value(load8(a.cs, c.pos + 1), c.pos, A + s);
         c.have_val = true;
         op_p = c.op; rs_p = c.rs; v_p = c.val;
       }
-      uint32_t word = 0;
-      bool emit = false;
-      if (valid) {
-        if (op == ':') {
-          emit = !(is_special(nx) && nx != ':' && !rs_e);
-          word = rs << 3 | v_self << 18;
-        } else if (is_special(op)) {
-          const bool merged = op_p == ':' && !rs;
-          emit = true;
-          word = opcode(op) | (merged ? rs_p : rs) << 3 | op_fields(load8(reinterpret_cast<const uint8_t*>(by), s + 1), sa, e) |
-                 (merged ? v_p : 0u) << 18;
-        } else {
-          const int64_t ol = e - sa;
-          emit = true;
-          word = 5u | rs << 3 | (uint32_t)(ol > 63 ? 63 : ol) << 4;
-        }
-      }
+      // branch-free unit word (tok_ref.c)
+      const bool merged = !colon && spc && op_p == ':' && !rs;
+      const bool absorbed = colon && special_lut(nx) && nx != ':' && !rs_e;
+      const bool emit = valid && !absorbed;
+      const uint32_t w_colon = rs << 3 | v_self << 18;
+      const uint32_t w_op = opcode(op) | (merged ? rs_p : rs) << 3 | op_fields_swar(v, len) | (merged ? v_p : 0u) << 18;
+      const uint32_t w_none = 5u | rs << 3 | (uint32_t)min(len + 1, 63) << 4;
+      const uint32_t word = colon ? w_colon : spc ? w_op : w_none;
       const uint64_t em = __ballot(emit);
       if (emit) ob[nout + lanes_below(em)] = word;
       nout += __popcll(em);

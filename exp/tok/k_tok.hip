@@ -128,19 +128,20 @@ __device__ __forceinline__ uint32_t lanes_below(uint64_t m) {
 // (v of the token before the step, for a ':' that the step's first unit absorbs)
 struct Carry { uint32_t op, rs, val; int64_t pos; bool have_val; };
 
-__global__ __launch_bounds__(kWaves * 64) void K_tok(TokArgs a) {
+#ifndef TOK_WPE
+#define TOK_WPE 4
+#endif
+__global__ __launch_bounds__(kWaves * 64) __attribute__((amdgpu_waves_per_eu(TOK_WPE))) void K_tok(TokArgs a) {
   constexpr int kStaged = 32 * kWords;                 // staged bytes: the step + a 64-byte halo
   __shared__ uint32_t s_rs[kWaves][kWords];             // read-start bits of the staged bytes
   __shared__ uint64_t s_by[kWaves][(kStaged + 16) / 8];  // the staged bytes (+ load8 overrun)
   __shared__ uint16_t s_list[kWaves][kStaged];           // token starts (step offsets), ascending
-  __shared__ uint32_t s_out[kWaves][kStep];              // the step's units (<= one per byte)
   const int l = lane(), wi = (int)threadIdx.x >> 6;
   const int64_t w = (int64_t)blockIdx.x * kWaves + wi;
   if (w >= a.nwaves) return;
   uint32_t* rsb = s_rs[wi];
   uint8_t* by = reinterpret_cast<uint8_t*>(s_by[wi]);
   uint16_t* list = s_list[wi];
-  uint32_t* ob = s_out[wi];
   const int64_t begin = w * a.S, end = begin + a.S < a.B ? begin + a.S : a.B;
   int64_t rn = a.wave_rn[w];
   // the token before `begin`: the last special byte within 32 bytes, or the
@@ -262,7 +263,7 @@ __global__ __launch_bounds__(kWaves * 64) void K_tok(TokArgs a) {
       const uint32_t w_none = 5u | rs << 3 | (uint32_t)min(len + 1, 63) << 4;
       const uint32_t word = colon ? w_colon : spc ? w_op : w_none;
       const uint64_t em = __ballot(emit);
-      if (emit) ob[nout + lanes_below(em)] = word;
+      if (emit) out[cnt + nout + lanes_below(em)] = word;  // contiguous across the round's lanes
       nout += __popcll(em);
       // carry to the next round / step: the round's last valid token
       const int lastl = (int)(n_own - 1 - j0 < 63 ? n_own - 1 - j0 : 63);
@@ -271,8 +272,6 @@ __global__ __launch_bounds__(kWaves * 64) void K_tok(TokArgs a) {
       c.val = bcast(v_self, lastl);
       c.have_val = true;
     }
-    wave_sync_lds();
-    for (uint32_t i = l; i < nout; i += 64) out[cnt + i] = ob[i];
     cnt += nout;
     wave_sync_lds();
   }

@@ -25,12 +25,13 @@ def main():
     ap.add_argument("--waves", type=int, default=8192)
     ap.add_argument("--reps", type=int, default=10)
     ap.add_argument("--check", default="c1,c2,c4")
+    ap.add_argument("--lib", default=os.path.join(HERE, "libtok.so"))
     args = ap.parse_args()
     import torch
     pkg = importlib.import_module("minion-plasmid-consensus_amd")
     eng = pkg.engine
     bench = importlib.import_module("bench")
-    lib = ctypes.CDLL(os.path.join(HERE, "libtok.so"))
+    lib = ctypes.CDLL(os.path.abspath(args.lib))
     lib.tok_launch.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]
     ref = ctypes.CDLL(os.path.join(HERE, "libtok_ref.so"))
@@ -68,7 +69,7 @@ def main():
         us = ts[len(ts) // 2]
         n_units = int(wcount.sum().item())
         alg = B + 4 * n_units + 8 * (N + 1)
-        rec = {"config": cfg, "reads": N, "cs_bytes": B, "waves": nw, "bytes_per_wave": S, "units": n_units,
+        rec = {"lib": os.path.basename(args.lib), "config": cfg, "reads": N, "cs_bytes": B, "waves": nw, "bytes_per_wave": S, "units": n_units,
                "median_us": us, "min_us": ts[0], "max_us": ts[-1], "algorithmic_bytes": alg,
                "GB_per_s": alg / us / 1e3, "units_per_cs_byte": n_units / max(B, 1)}
         if cfg in args.check.split(","):

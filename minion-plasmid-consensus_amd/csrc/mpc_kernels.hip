@@ -579,6 +579,13 @@ __device__ __forceinline__ void chunk_store(uint8_t* p, U8x32 v) {
   reinterpret_cast<uint4*>(p)[1] = v.b;
 }
 
+// events per thread per staged scatter chunk of the epilogue's bucket sort:
+// 12 -> one chunk per workgroup at C2 (parse phase 8 -> 12: C2 143.5 -> 141.9
+// us, C4 -0.7 %, C5 -0.9 %, C3 -0.3 %, C1 +0.8 %; 16 the same;
+// profiles/r04_experiments/kparse_epilogue_chunk.txt)
+#ifndef MPC_EPI_U
+#define MPC_EPI_U 12
+#endif
 // End of a parse workgroup: flush the LDS position
 // tallies and the LEFT-gap bitmap with contiguous atomics, then bucket-sort the
 // workgroup's insertion events by gap (counting sort, kBW gaps per bucket) from
@@ -627,7 +634,7 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, int64
   uint32_t* bcur = uni;
   const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;
   const int bstride = (int)blockDim.x;
-  constexpr int kEpiU = 8;  // events per thread per staged scatter chunk
+  constexpr int kEpiU = MPC_EPI_U;  // events per thread per staged scatter chunk
   if (threadIdx.x < 64) {  // exclusive scan over buckets by one wave
     int carry_b = 0;
     for (int c0 = 0; c0 < nbk; c0 += 64) {

@@ -93,13 +93,18 @@ class DistExchange:
             d.all_reduce(t, op=d.ReduceOp.MAX, group=self.group)
         elif op == "or":
             # RCCL has no bitwise reduction: gather the bitmaps, OR them as a tree
+            # (a fresh output per call: one exchange may serve pipelines on several streams)
             st = self._gather_rows(t)
             k = self.world
-            while k > 1:
+            while k > 2:
                 h = (k + 1) // 2  # rows [h, k) fold onto [0, k - h)
                 st[: k - h] |= st[h:k]
                 k = h
-            t.copy_(st[0])
+            if k == 2:
+                import torch
+                torch.bitwise_or(st[0], st[1], out=t)  # the last fold straight into t
+            else:
+                t.copy_(st[0])
         else:
             raise ValueError(op)
 

@@ -2237,9 +2237,24 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
   MPC_STAMP(st_prev);
 #endif
   const int64_t nunits = (a.status[MPC_ST_FLAGS] & DE_INTERNAL) ? 0 : a.status[MPC_ST_UNITS];
-  for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+  // 512-thread blocks (plans with many small buckets, C5): the tallies are
+  // zeroed once and every unit flushes (and re-zeroes) only the runs it can
+  // touch (s_kn), and short slices are searched for all events at once -- C5
+  // K_left 215 -> 189 us; on the 1024-thread plans (C2-C4) the same code was
+  // slower (profiles/r04_experiments/k_left_variants.txt: l_kfpa)
+  constexpr bool kLean = UB == 512;
+  __shared__ int32_t s_kn;
+  if constexpr (kLean) {
     for (int k = threadIdx.x; k < kBW * kMs; k += blockDim.x) Ml[k] = 0;
     for (int k = threadIdx.x; k < kBW * kTs; k += blockDim.x) Tl[k] = 0;
+  }
+  for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
+    if constexpr (kLean) {
+      if (threadIdx.x == 0) s_kn = 0;  // ordered before its atomics by load_unit's barriers
+    } else {
+      for (int k = threadIdx.x; k < kBW * kMs; k += blockDim.x) Ml[k] = 0;
+      for (int k = threadIdx.x; k < kBW * kTs; k += blockDim.x) Tl[k] = 0;
+    }
     MPC_LSEG(0);
     const UnitView uv = load_unit<false>(a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, a.right_start, a.rsl,
                                          a.roff, nullptr, nullptr, nullptr, a.pwork, s_r0, s_pre, s_src, s_wsum, s_rs,
@@ -2255,16 +2270,39 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     // searched once, then advanced; with short slices (C2) every event's search
     // is independent (a chain of advancing searches would serialize them)
     const bool adv = s_pre[256] >= UB * uv.nsl;
-    int js = -1;
+    if (kLean && !adv) {
+      // short slices: every event's slice by a branch-free 8-step binary
+      // search over the 256 slices (the last j with s_pre[j] <= e), the kEPT
+      // searches interleaved -- 8 dependent LDS round trips per unit
 #pragma unroll
-    for (int q = 0; q < kEPT; ++q) {
-      const int e = uv.e0 + (int)threadIdx.x + q * UB;
-      evs[q] = ~0u;
-      jsq[q] = 0;
-      if (e < uv.e0 + uv.cnt) {
-        js = unit_slice_next(s_pre, e, adv ? js : -1);
-        jsq[q] = js;
-        evs[q] = a.ins_sorted[s_src[js] + (e - s_pre[js])];
+      for (int q = 0; q < kEPT; ++q) jsq[q] = 0;
+#pragma unroll
+      for (int h = 128; h >= 1; h >>= 1) {
+#pragma unroll
+        for (int q = 0; q < kEPT; ++q) {
+          const int e = uv.e0 + (int)threadIdx.x + q * UB;
+          const int m = jsq[q] + h;
+          jsq[q] = s_pre[m] <= e ? m : jsq[q];
+        }
+      }
+#pragma unroll
+      for (int q = 0; q < kEPT; ++q) {
+        const int e = uv.e0 + (int)threadIdx.x + q * UB;
+        evs[q] = ~0u;
+        if (e < uv.e0 + uv.cnt) evs[q] = a.ins_sorted[s_src[jsq[q]] + (e - s_pre[jsq[q]])];
+      }
+    } else {
+      int js = -1;
+#pragma unroll
+      for (int q = 0; q < kEPT; ++q) {
+        const int e = uv.e0 + (int)threadIdx.x + q * UB;
+        evs[q] = ~0u;
+        jsq[q] = 0;
+        if (e < uv.e0 + uv.cnt) {
+          js = unit_slice_next(s_pre, e, adv ? js : -1);
+          jsq[q] = js;
+          evs[q] = a.ins_sorted[s_src[js] + (e - s_pre[js])];
+        }
       }
     }
     // the run of an event at a mixed gap is a search of the gap's RIGHT reads:
@@ -2273,6 +2311,14 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     const int32_t v0 = s_rsl[0], vn = s_rsl[uv.gl + 1 - g0] - v0;
     const bool vl = vn <= kLV;
     for (int k = threadIdx.x; vl && k < vn; k += blockDim.x) s_vals[k] = a.vals_out[v0 + k];
+    if constexpr (kLean) {
+      // LDS runs this unit can touch: an event at gap p has run k in
+      // [roff, roff + its mixed RIGHT reads]; the flush covers runs < s_kn
+      if (threadIdx.x < kBW && (int)threadIdx.x <= uv.gl - g0) {
+        const int p = (int)threadIdx.x, k0 = s_roff[p];
+        if (k0 < kKMax) atomicMax(&s_kn, min(k0 + s_rsl[p + 1] - s_rsl[p], kKMax - 1) + 1);
+      }
+    }
     MPC_LSEG(2);
     __syncthreads();
     MPC_LSEG(3);
@@ -2317,6 +2363,28 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     MPC_LSEG(4);
     __syncthreads();
     MPC_LSEG(5);
+    if constexpr (kLean) {  // runs k < s_kn of every gap (k-major), read and re-zeroed
+      const int kn = s_kn;
+      for (int q = threadIdx.x; q < kBW * kn; q += blockDim.x) {
+        const int p = q & (kBW - 1), k = q / kBW;
+        const uint32_t m = Ml[p * kMs + k];
+        if (m) {
+          atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + k, (int32_t)m);
+          Ml[p * kMs + k] = 0;
+        }
+      }
+      for (int q = threadIdx.x; q < kBW * kn * 16; q += blockDim.x) {  // contiguous per (gap, run)
+        const int p = (q >> 4) & (kBW - 1), k = q / (kBW * 16);
+        const uint32_t v = Tl[p * kTs + k * 16 + (q & 15)];
+        if (v) {
+          atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + k) * 16 + (q & 15), v);
+          Tl[p * kTs + k * 16 + (q & 15)] = 0;
+        }
+      }
+      __syncthreads();
+      MPC_LSEG(6);
+      continue;
+    }
 #ifdef MPC_ABL_LEFT_NOFLUSH  // timing ablation only (wrong results): no unit flush
     for (int q = threadIdx.x; q < 0; q += blockDim.x) {
 #else

@@ -245,9 +245,43 @@ def kernel_roofline(pkg, eng, cfg, reps, torch):
     return out
 
 
+def launch_ranks(n, argv):
+    """``bench.py --gpus N`` (N > 1) started WITHOUT a launcher: run the same
+    command as N rank processes (one per GPU) under torch.distributed.run, as a
+    child of this process, and return its exit status.  This process never
+    touches the GPU (nothing HIP is initialised before the children start; the
+    JSON line is printed by rank 0 of the children)."""
+    import socket
+    import subprocess
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + list(argv)
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC only on this pool (RCCL)
+    return subprocess.call(cmd, env=env)
+
+
+def world_from_env(gpus):
+    """(world, launched): the rank count of this run.  Under a launcher it is
+    WORLD_SIZE, which must equal ``--gpus`` when that is given; without one it
+    is 1 (``--gpus N > 1`` self-launches first, see launch_ranks)."""
+    if "WORLD_SIZE" in os.environ:
+        world = int(os.environ["WORLD_SIZE"])
+        if gpus is not None and gpus != world:
+            raise SystemExit(f"bench.py: --gpus {gpus} but the launcher started WORLD_SIZE={world} ranks")
+        return world, True
+    if gpus is not None and gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1, got {gpus}")
+    return 1, False
+
+
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one rank each); without a launcher, N > 1 starts N ranks itself "
+                         "(torch.distributed.run); under one it must equal WORLD_SIZE")
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
@@ -259,18 +293,28 @@ def main():
                     help="CUs the parse grid is sized for with batches in flight (default: per config)")
     ap.add_argument("--dist", action="store_true",
                     help="take the distributed path (process group + dist.DistExchange) even at WORLD_SIZE=1")
-    ap.add_argument("--graph", action="store_true",
-                    help="distributed path: replay every pipeline's step from a HIP graph (no host dispatch)")
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+                    help="distributed path: replay every pipeline's step from a HIP graph (no host dispatch); "
+                         "auto = on for RCCL at world size > 1")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
-    ap.add_argument("--hbm-config", default="c3",
-                    help="also time K_parse on this (L3-exceeding) config for the HBM roofline; '' to skip")
-    args = ap.parse_args()
+    ap.add_argument("--hbm-config", default="c3", type=lambda s: s.strip().lower(),
+                    help="also time K_parse on this (L3-exceeding) config for the HBM roofline; "
+                         "'' or 'none' to skip")
+    argv = sys.argv[1:]
+    args = ap.parse_args(argv)
+    if args.hbm_config in ("", "none"):
+        args.hbm_config = ""
+    elif args.hbm_config not in CONFIGS:
+        ap.error(f"--hbm-config {args.hbm_config!r}: not one of {sorted(CONFIGS)} (or '' / none)")
+
+    world, launched = world_from_env(args.gpus)
+    if not launched and (args.gpus or 1) > 1:
+        sys.exit(launch_ranks(args.gpus, argv))
 
     import torch
     import torch.distributed as dist
 
-    world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     # one rank per GPU; the modulo only matters for rehearsals with more ranks than GPUs
@@ -346,10 +390,16 @@ def main():
     # step costs no host dispatch (world size 1 over RCCL, C2: eager 220 us /
     # step with 141 us of host dispatch, replay 202.5 us = the local runner;
     # profiles/r04_experiments/dist_graph_world1.txt).  All ranks capture the
-    # same sequence; if any rank fails to, every rank stays eager.  Opt-in: the
-    # capture of RCCL collectives has run at world size 1 only (one GPU here).
+    # same sequence; if any rank fails to, every rank stays eager.  Default at
+    # world size > 1 over RCCL (where the eager step's host dispatch and four
+    # collectives would otherwise sit on every rank's critical path); parity of
+    # the replayed step is pinned by tests/test_dist_gpu.py::test_rccl_world1_*.
+    # gloo (host-staged tensors) cannot be captured: always eager.
     graph_note = None
-    if args.graph and use_dist and cfg != "c5":
+    want_graph = args.graph == "on" or (args.graph == "auto" and world > 1 and backend == "nccl")
+    if args.graph == "on" and backend != "nccl":
+        graph_note, want_graph = "graph replay needs RCCL (host-staged gloo exchanges): eager steps", False
+    if want_graph and use_dist and cfg != "c5":
         graphs, ok = [], 1
         try:
             for r in runners:

@@ -134,6 +134,14 @@ enum {
 };
 
 int mpc_version(void);
+/* Measurement switches this library was compiled with (0 in the product
+ * build, tests/test_abi.py): MPC_BF_STAMPS s_memtime stamp build, MPC_BF_TUNING
+ * planner overrides from the environment, MPC_BF_VARIANT a kernel variant
+ * (a tuning macro set on the compiler command line). */
+#define MPC_BF_STAMPS 1
+#define MPC_BF_TUNING 2
+#define MPC_BF_VARIANT 4
+int mpc_build_flags(void);
 const char* mpc_last_error(void);
 
 /* Plan for one input shape.  row_cap = capacity of the pileup-row buffers; the

@@ -35,6 +35,27 @@
 #include "mpc.h"
 #include "mpc_device.h"
 
+// What this library was compiled with (mpc_build_flags): product builds set
+// none of the measurement switches below on the command line.  Recorded before
+// the #ifndef defaults further down give them their product values.
+#if defined(MPC_STAMPS) || defined(MPC_STAMPS_LEFT)
+#define MPC_BF_STAMPS_ 1
+#else
+#define MPC_BF_STAMPS_ 0
+#endif
+#if defined(MPC_TUNING_OVERRIDES)
+#define MPC_BF_TUNING_ 2
+#else
+#define MPC_BF_TUNING_ 0
+#endif
+#if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
+    defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) || defined(MPC_FLANK_BYTES4) ||     \
+    defined(MPC_FLANK_BLOCKS_MAX)
+#define MPC_BF_VARIANT_ 4
+#else
+#define MPC_BF_VARIANT_ 0
+#endif
+
 using namespace mpc;
 
 namespace {
@@ -868,9 +889,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int64_t sev_base = (P - a.cs_base) / 3 + 2 * ra;  // ... and its substitution-event regions (TM 3)
   uint32_t nsub_v = 0;                                    // lane k: substitution events of window k
   uint32_t nev = 0;                                       // events written (wave-uniform)
-#ifdef MPC_ABL_TOKENIZE_ONLY
-  uint32_t nunit = 0;  // timing ablation: decoded units written (pass-1 cost of a split parse)
-#endif
   int64_t rs0 = ra;         // first read whose cs starts at or after P
   bool carry = false;       // slot 0 holds a read continuing into this window
   int32_t c_base = 0;       // ... and its coordinate base (wave-uniform): i = base + window prefix of advances
@@ -1075,10 +1093,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const int q = qc + lanes_below(brs) + (is_rs ? 1 : 0);
       // the read's slot (tstart, read, i_end), loaded before the decode
       const int32_t q_ts = W.s_ts[q], q_read = W.s_read[q], q_iend = W.s_iend[q];
-#ifdef MPC_ABL_NODECODE  // timing ablation only (wrong results): no decode
-      int adv0 = 0, adv = (s0 & 7) == 0 ? 1 : 0, kind = v ? 2 : 0, olen_e = 2;
-      uint32_t pay = (uint32_t)s0 & 3u, err = 0;
-#else
       // ---- decode.  Fast path: every unit of the round is canonical -- an
       // optional absorbed ':' prefix of 1-4 digits, then ':' + 1-4 digits, '*' +
       // 1-4 bytes ending in a base, '+' + 1-4 bases or '-' + 1-4 bytes, ending
@@ -1201,15 +1215,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
           }
         }
       }
-#endif
       MPC_SEG(2);
-#ifdef MPC_ABL_TOKENIZE_ONLY  // timing ablation only (wrong results): decode, one packed word per unit, no effects
-      if (v) a.ins_raw[ev_base + nunit + l] = (uint64_t)(uint32_t)(adv0 + adv) | ((uint64_t)kind << 32) |
-                                              ((uint64_t)pay << 40) | ((uint64_t)(olen_e & 0xffff) << 48) | (uint64_t)err;
-      nunit += (uint32_t)__popcll(ballot(v));
-      qc += __popcll(brs);
-      continue;
-#endif
       // ---- coordinates ----
       const int advu = adv0 + adv;            // unit advance <= 2^23: 64 lanes stay < 2^29
       const int ainc = wave_scan_i32(advu);
@@ -1244,11 +1250,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const bool bad_i = ((adv0 > 0) & ((iu | (n - i)) < 0)) | (((uint32_t)(kind - 1) <= 2u) & ((i | (n - adv - i)) < 0));
       uint32_t te = err | (bad_i ? DE_INDEX : 0u);
       const int rl = q_read;
-#ifdef MPC_ABL_NOEFFECTS  // timing ablation only (wrong results): no tallies / events
-      const bool ok = false;
-#else
       const bool ok = te == 0;
-#endif
       if (ok & (kind == 2) & (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
       const bool del = ok & (kind == 4) & (i >= 0) & (i < n);
       if (del) {
@@ -1422,11 +1424,7 @@ __global__ __launch_bounds__(1024) void K_subs(SubsArgs a) {
   uint32_t* dst = a.sub + ((int64_t)a.gbase[smp] + p0) * 4;
   for (int j = threadIdx.x; j < kSubWin * 4; j += blockDim.x) {  // consecutive lanes, consecutive words
     const uint32_t x = (cnt[j >> 1] >> (16 * (j & 1))) & 0xffffu;
-#ifdef MPC_ABL_SUBS_NOFLUSH  // timing ablation only (wrong results): no flush
-    if (x == 0xfffffu) atomicAdd(dst + j, x);
-#else
     if (x && p0 + (j >> 2) < n) atomicAdd(dst + j, x);
-#endif
   }
 }
 
@@ -1740,9 +1738,7 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
 #pragma unroll
     for (int u = 0; u < kRegE; ++u) e[u] = s0 + 64 * u + l < s1 ? pool[s0 + 64 * u + l] : 0u;
     __syncthreads();  // every wave holds its entries before the first scatter
-#ifndef MPC_ABL_RSORT_NOPASS  // timing ablation only (wrong order): no sort passes
     for (int p = 0; p < passes; ++p) rsort_reg_pass(e, s0, s1, sb + 8 * p, pool, wc, hb, p + 1 < passes);
-#endif
     const uint32_t im = (1u << sb) - 1u;  // (sb <= 15 here)
     for (int64_t i0 = 0; i0 < M; i0 += 4 * kRS) {
       uint32_t x[4];
@@ -1750,11 +1746,7 @@ __global__ __launch_bounds__(kRS) void K_rsort(Dev d, int32_t nblocks, int32_t e
       for (int u = 0; u < 4; ++u) { const int64_t i = i0 + tid + u * kRS; x[u] = i < M ? pool[i] : 0u; }
       int32_t vv[4];
 #pragma unroll
-#ifdef MPC_ABL_RSORT_NOVALS  // timing ablation only (wrong values): no value gather
-      for (int u = 0; u < 4; ++u) vv[u] = (int32_t)(x[u] & im) & 0;
-#else
       for (int u = 0; u < 4; ++u) { const int64_t i = i0 + tid + u * kRS; vv[u] = i < M ? d.vals_tmp[x[u] & im] : 0; }
-#endif
 #pragma unroll
       for (int u = 0; u < 4; ++u) {
         const int64_t i = i0 + tid + u * kRS;
@@ -2385,20 +2377,12 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       MPC_LSEG(6);
       continue;
     }
-#ifdef MPC_ABL_LEFT_NOFLUSH  // timing ablation only (wrong results): no unit flush
-    for (int q = threadIdx.x; q < 0; q += blockDim.x) {
-#else
     for (int q = threadIdx.x; q < kBW * kKMax; q += blockDim.x) {
-#endif
       const int k = q % kKMax, p = q / kKMax;
       const uint32_t m = Ml[p * kMs + k];
       if (m) atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + k, (int32_t)m);
     }
-#ifdef MPC_ABL_LEFT_NOFLUSH
-    for (int q = threadIdx.x; q < 0; q += blockDim.x) {
-#else
     for (int q = threadIdx.x; q < kBW * kKMax * 16; q += blockDim.x) {  // contiguous per (gap, run)
-#endif
       const int k = (q >> 4) % kKMax, p = (q >> 4) / kKMax;
       const uint32_t v = Tl[p * kTs + k * 16 + (q & 15)];
       if (v) atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + k) * 16 + (q & 15), v);
@@ -2419,11 +2403,7 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     atomicMax(a.M + run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + o.read), o.len);
   }
   // upstream flanks (block-uniform trips: block_atomic_max synchronizes the block)
-#ifdef MPC_ABL_LEFT_NOREADS  // timing ablation only (wrong results): no per-read pass
-  for (int64_t r0 = fb * blockDim.x; r0 < 0; r0 += nthreads) {
-#else
   for (int64_t r0 = fb * blockDim.x; r0 < a.N; r0 += nthreads) {
-#endif
     const int64_t r = r0 + threadIdx.x;
     int64_t run = 0;
     int32_t L = 0;
@@ -2850,11 +2830,7 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
       const int cn32 = (int)cn, c032 = (int)c0;
       const int32_t w032 = w0 >= 0 ? (int32_t)w0 : -(1 << 30);  // no window: never a hit
       const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
-#ifdef MPC_ABL_FLANK_NOBYTES  // timing ablation only (wrong results): no per-byte tallies
-      for (int x4 = 4 * tid; x4 < 0; x4 += 4 * (int)blockDim.x) {
-#else
       for (int x4 = 4 * tid; x4 < cn32; x4 += 4 * (int)blockDim.x) {
-#endif
         const uint32_t word = bm[x4 >> 5];  // (the 4 bytes share a bitmap word)
         const int ob = wpre[x4 >> 5];
         const int q = x4 + sh0;             // stage offset (+16 padding: the second dword is in bounds)
@@ -2885,11 +2861,7 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
       // 32-bit: rows < row_cap < 2^31, a block's flank bytes < 2^31
       const int cn32 = (int)cn, c032 = (int)c0;
       const int32_t w032 = w0 >= 0 ? (int32_t)w0 : -(1 << 30);  // no window: never a hit
-#ifdef MPC_ABL_FLANK_NOBYTES  // timing ablation only (wrong results): no per-byte tallies
-      for (int x = tid; x < 0; x += blockDim.x) {
-#else
       for (int x = tid; x < cn32; x += blockDim.x) {
-#endif
         const uint32_t word = bm[x >> 5];
         const int o = wpre[x >> 5] + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
         const int32_t rw = t_row[o];
@@ -2910,11 +2882,7 @@ __global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
     const int64_t w0 = s_w0[side];
     for (int k = tid; k < kWinRows * 4; k += blockDim.x) {
       const uint32_t v = win[side][(k >> 2) * 5 + (k & 3)];
-#ifdef MPC_ABL_FLANK_NOFLUSH  // timing ablation only (wrong results): no window flush
-      if (v == 0xfffffffu) atomicAdd(a.rows + w0 * 4 + k, v);
-#else
       if (v) atomicAdd(a.rows + w0 * 4 + k, v);
-#endif
     }
   }
   if (lerr) {
@@ -3373,6 +3341,8 @@ static inline unsigned nblk(int64_t n, int b = 256) {
 extern "C" {
 
 int mpc_version(void) { return MPC_ABI_VERSION; }
+
+int mpc_build_flags(void) { return MPC_BF_STAMPS_ | MPC_BF_TUNING_ | MPC_BF_VARIANT_; }
 
 size_t mpc_input_layout(size_t* off, int cap) {
 #define MPC_F(f) offsetof(mpc_input, f)

@@ -129,8 +129,10 @@ def run_case(name, script, core, repeats=1, golden=True):
     wall = ws[len(ws) // 2] if len(ws) % 2 else 0.5 * (ws[len(ws) // 2 - 1] + ws[len(ws) // 2])
     frac = (b - a) / full
     return cfg, {
-        "value": aligned / wall, "unit": "aligned bases/s", "cores": 1, "kind": "reference",
-        "value_best": aligned / ws[0], "wall_min_s": round(ws[0], 3),
+        # value = the FASTEST run: the build container shares its host, so the
+        # slower runs measure the neighbours; the median is kept
+        "value": aligned / ws[0], "unit": "aligned bases/s", "cores": 1, "kind": "reference",
+        "value_best": aligned / ws[0], "value_median": aligned / wall, "wall_min_s": round(ws[0], 3),
         "wall_s": round(wall, 3), "walls_s": [round(w, 3) for w in walls], "repeats": len(walls),
         "spread": round((ws[-1] - ws[0]) / wall, 4),
         "aligned_bases": aligned, "strand_jobs": strands,
@@ -138,7 +140,7 @@ def run_case(name, script, core, repeats=1, golden=True):
         "sample": (f"{name}: reads [{a}, {b}) of the {full}-read {cfg} set ({100 * frac:g} %), "
                    f"{strands} strand job(s) run one after the other (Snakefile:401-423), "
                    f"/root/reference/src/mapped_paf_read_parser.py whole script, taskset -c {core}, "
-                   f"median of {len(walls)} run(s)"
+                   f"value = the fastest of {len(walls)} run(s) (min wall; value_median = the median)"
                    + ("; rate extrapolated linearly to the full set (SURVEY §8(d))" if frac < 1.0 else "")),
     }
 
@@ -177,13 +179,15 @@ def run_all_cores(script, cores, repeats, reads=1000):
             print(f"c5 all cores rep{rep}: {wall:.2f} s", flush=True)
     ws = sorted(walls)
     wall = ws[len(ws) // 2]
-    return {"value": aligned / wall, "value_best": aligned / ws[0], "unit": "aligned bases/s", "cores": len(cores),
+    return {"value": aligned / ws[0], "value_best": aligned / ws[0], "value_median": aligned / wall,
+            "unit": "aligned bases/s", "cores": len(cores),
             "kind": "reference", "wall_s": round(wall, 3), "wall_min_s": round(ws[0], 3),
             "walls_s": [round(w, 3) for w in walls], "repeats": len(walls), "spread": round((ws[-1] - ws[0]) / wall, 4),
             "aligned_bases": aligned, "extrapolated": True,
             "sample": (f"c5 on all {len(cores)} host cores: {len(cores)} reference processes started together, one per "
                        f"core (taskset), each one plasmid (seeds 5000..{4999 + len(cores)}) with reads [0, {reads}) of "
-                       f"its 10k and both strand jobs one after the other; median of {len(walls)} batch(es); rate "
+                       f"its 10k and both strand jobs one after the other; value = the fastest of {len(walls)} batch(es) (median: "
+                       f"value_median); rate "
                        "extrapolated linearly to the full set (SURVEY §8(d))")}
 
 

@@ -206,3 +206,14 @@ def test_one_hip_runtime_either_order(order):
             "%s; print(len(e._hip_runtime_paths()), t)" % (REPO, steps))
     out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, check=True).stdout.split()
     assert out == ["1", "False"], out
+
+
+def test_product_build_flags(pkg):
+    """The shipped libmpc.so is the product build: no stamps, no planner
+    overrides, no kernel variant macro (the timing ablations
+    live in exp/ablations.patch, not in the product source)."""
+    lib = pkg.engine.lib()
+    lib.mpc_build_flags.restype = ctypes.c_int
+    assert lib.mpc_build_flags() == 0
+    src = open(os.path.join(REPO, "minion-plasmid-consensus_amd", "csrc", "mpc_kernels.hip")).read()
+    assert "MPC_ABL_" not in src and "wrong results" not in src

@@ -118,7 +118,9 @@ def test_c3_eight_shards_in_process(pkg):
 
 def _nccl_worker(port, q):
     """ONE rank on cuda:0 over RCCL ("nccl"): two ShardedPileups in flight on
-    one communicator, on two streams (bench.py --dist --inflight 2 at N=1)."""
+    two streams, each with its OWN communicator (dist.new_group per pipeline,
+    exactly as bench.py builds them), stepped eagerly and then replayed from
+    one HIP graph per pipeline (bench.py's default at N > 1 over RCCL)."""
     try:
         os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
         import torch
@@ -130,9 +132,10 @@ def _nccl_worker(port, q):
             dmod = importlib.import_module("minion-plasmid-consensus_amd.dist")
             bench = importlib.import_module("bench")
             samples, _ = bench.shard_samples(pkg, "c2", 0, 1)
-            ex = dmod.DistExchange()
-            assert not ex.host_staged  # device tensors in place: the RCCL branches of dist.py
-            sps = [dmod.ShardedPileup([samples], [0], ex=ex) for _ in range(2)]
+            groups = [tdist.new_group([0]) for _ in range(2)]
+            exs = [dmod.DistExchange(g) for g in groups]
+            assert not any(ex.host_staged for ex in exs)  # device tensors in place: the RCCL branches
+            sps = [dmod.ShardedPileup([samples], [0], ex=ex) for ex in exs]
             streams = [torch.cuda.current_stream(), torch.cuda.Stream()]
             out = []
             for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
@@ -143,7 +146,34 @@ def _nccl_worker(port, q):
                 torch.cuda.synchronize()
                 for k in (0, 1):
                     sps[k].check()
-                    out.append((mdf, gtf, k, [dict(r) for r in sps[k].fetch()]))
+                    out.append((mdf, gtf, k, "eager", [dict(r) for r in sps[k].fetch()]))
+            # graph replay, as bench.py captures it: warm step on the capture
+            # stream, then the captured step; replayed twice on the pipelines' streams
+            mdf, gtf = 0.1, 5.0
+            graphs = []
+            for sp in sps:
+                g = torch.cuda.CUDAGraph()
+                cap = torch.cuda.Stream()
+                with torch.cuda.stream(cap):
+                    sp.step(mdf, gtf)
+                    cap.synchronize()
+                    with torch.cuda.graph(g, stream=cap):
+                        sp.step(mdf, gtf)
+                graphs.append(g)
+            torch.cuda.synchronize()
+            # a full-pileup step in between, so the replay must rewrite every output
+            for k in (0, 1):
+                sps[k].step(-1.0, 1.0)
+            torch.cuda.synchronize()
+            for rep in range(2):
+                for k in (0, 1):
+                    with torch.cuda.stream(streams[k]):
+                        graphs[k].replay()
+            torch.cuda.synchronize()
+            for k in (0, 1):
+                sps[k].check()
+                out.append((mdf, gtf, k, "graph", [dict(r) for r in sps[k].fetch()]))
+            del graphs
             q.put((out, None))
         finally:
             tdist.destroy_process_group()
@@ -174,7 +204,32 @@ def test_rccl_world1_two_pipelines(pkg):
     bench = importlib.import_module("bench")
     samples, _ = bench.shard_samples(pkg, "c2", 0, 1)
     full = du.oracle_many(samples, -1.0, 1.0)
-    assert len(out) == 4
-    for mdf, gtf, k, got in out:
+    assert len(out) == 6
+    for mdf, gtf, k, how, got in out:
         for s, (g, f) in enumerate(zip(got, full)):
-            du.compare(g, du.derive(f, mdf, gtf), ("rccl1", k, s, mdf))
+            du.compare(g, du.derive(f, mdf, gtf), ("rccl1", how, k, s, mdf))
+
+
+@pytest.mark.timeout(600)
+def test_bench_self_launch_two_ranks(tmp_path):
+    """``python bench.py --gpus 2`` with no launcher starts 2 rank processes
+    itself (torch.distributed.run as a child) -- here rehearsed on one GPU over
+    gloo -- and rank 0's JSON line reports n_gpus == 2."""
+    import json
+    import subprocess
+    import sys
+    repo = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    env["MPC_DIST_BACKEND"] = "gloo"
+    cmd = [sys.executable, os.path.join(repo, "bench.py"), "--gpus", "2", "--config", "c2", "--steps", "3",
+           "--warmup", "1", "--kernel-reps", "2", "--inflight", "2", "--hbm-config", ""]
+    p = subprocess.run(cmd, env=env, cwd=str(tmp_path), capture_output=True, text=True, timeout=540)
+    assert p.returncode == 0, p.stderr[-4000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-4000:]
+    rec = json.loads(lines[0])
+    assert rec["n_gpus"] == 2
+    assert rec["config"]["parallelism"] == "read-shardx2"
+    assert rec["config"]["process_group"] == "gloo"
+    assert rec["config"]["global_reads_per_sample"] == 200_000  # weak scaling: 2 x 100k
+    assert rec["value"] > 0

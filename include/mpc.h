@@ -56,6 +56,19 @@ extern "C" {
 #define MPC_DE_KEY 8u      /* written base not in ACGT (KeyError, :61 / :71) */
 #define MPC_DE_CAPACITY 16u /* row capacity too small: re-plan with status[MPC_ST_ROWS_NEEDED] */
 #define MPC_DE_INTERNAL 32u /* invariant violated (bug) */
+#define MPC_DE_UNSUPPORTED 64u /* input the reference accepts but this engine does not: a negative target
+                                  start whose upstream flank, '+' insertion or downstream flank Python's
+                                  negative index wrap would write into an ODD (reference-base) position
+                                  (tests/golden/n_neg_ins, n_neg_flank, n_neg_end); tstart < MPC_TSTART_MIN */
+
+/* Lowest target start the engine takes.  Negative starts (minimap2 never
+ * writes one) follow the reference's Python negative indexing (:222,
+ * :300-303): matches and deletions below 0 write nothing, a '*' below 0 writes
+ * a one-base LEFT string at gap n + 1 + i, an index below -(2n+1) raises
+ * IndexError; a write into a wrapped odd position is MPC_DE_UNSUPPORTED. */
+#ifndef MPC_TSTART_MIN
+#define MPC_TSTART_MIN (-(1 << 28))
+#endif
 
 /* status words (uint32) at buffer MPC_BUF_STATUS */
 #define MPC_ST_FLAGS 0       /* OR of MPC_DE_* */
@@ -76,7 +89,7 @@ typedef struct {
   const int64_t* ref_off;  /* [n_samples+1] offsets into ref */
   const uint8_t* cs;       /* cs tag text after "cs:" (e.g. "Z::120*ag:7+tt"), concatenated (:231-234) */
   const int64_t* cs_off;   /* [n_reads+1]; the cs buffer must stay readable up to cs_off[n_reads]+2048 */
-  const int32_t* tstart;   /* [n_reads] PAF column 8, target start (:222) */
+  const int32_t* tstart;   /* [n_reads] PAF column 8, target start (:222); >= MPC_TSTART_MIN */
   const uint8_t* up;       /* upstream flanks (read bases before the alignment, :264); up and down
                               must stay readable 16 bytes past their last offset */
   const int64_t* up_off;   /* [n_reads+1] */

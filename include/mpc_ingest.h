@@ -36,6 +36,10 @@ extern "C" {
 #define MPC_INGEST_OK 0
 #define MPC_INGEST_ERROR 1
 #define MPC_INGEST_FALLBACK 2
+/* lowest PAF target start passed on to the engine (same value as mpc.h) */
+#ifndef MPC_TSTART_MIN
+#define MPC_TSTART_MIN (-(1 << 28))
+#endif
 
 typedef struct {
   uint8_t* ref;         /* concatenated, rstrip()ed, upper-cased reference (:163-165) */

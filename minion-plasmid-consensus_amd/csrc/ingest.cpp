@@ -690,7 +690,7 @@ void job_pack(Job& J, int T, mpc_ingest_out* out) {
                                           " not in the reads file)");
       return;
     }
-    if (r.ts < 0 || r.ts >= ((int64_t)1 << 31)) {
+    if (r.ts < MPC_TSTART_MIN || r.ts >= ((int64_t)1 << 31)) {  // negative: wrapped on the device (mpc.h)
       J.fail.set(MPC_INGEST_ERROR, 0, "target start out of range (unsupported)");
       return;
     }

@@ -50,7 +50,7 @@
 #endif
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) || defined(MPC_FLANK_BYTES4) ||     \
-    defined(MPC_FLANK_BLOCKS_MAX)
+    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -61,7 +61,8 @@ using namespace mpc;
 namespace {
 
 constexpr uint32_t DE_OP = MPC_DE_OP, DE_VALUE = MPC_DE_VALUE, DE_INDEX = MPC_DE_INDEX,
-                   DE_KEY = MPC_DE_KEY, DE_CAP = MPC_DE_CAPACITY, DE_INTERNAL = MPC_DE_INTERNAL;
+                   DE_KEY = MPC_DE_KEY, DE_CAP = MPC_DE_CAPACITY, DE_INTERNAL = MPC_DE_INTERNAL,
+                   DE_UNSUP = MPC_DE_UNSUPPORTED;
 
 constexpr int kBlk = 1024;          // cs bytes staged per wave iteration (64 lanes x 16 B)
 constexpr int kInsInline = 4;       // insertions up to this length travel as one event word
@@ -323,14 +324,22 @@ template <int TM> constexpr bool fast_decode() { return (MPC_FAST_DECODE_MODES >
 #ifndef MPC_LDS_BASE_MODES
 #define MPC_LDS_BASE_MODES 0x07
 #endif
-template <int TM> constexpr bool lds_base() { return (MPC_LDS_BASE_MODES >> TM) & 1; }
-__host__ __device__ constexpr bool lds_base_rt(int tm) { return (MPC_LDS_BASE_MODES >> tm) & 1; }
+// ... or by one ds_bpermute from the round's last read-start lane (no LDS slot,
+// no fence; takes precedence over the two above)
+#ifndef MPC_BPERM_BASE_MODES
+#define MPC_BPERM_BASE_MODES 0x00
+#endif
+template <int TM> constexpr bool bperm_base() { return (MPC_BPERM_BASE_MODES >> TM) & 1; }
+template <int TM> constexpr bool lds_base() { return !bperm_base<TM>() && ((MPC_LDS_BASE_MODES >> TM) & 1); }
+__host__ __device__ constexpr bool lds_base_rt(int tm) {
+  return !((MPC_BPERM_BASE_MODES >> tm) & 1) && ((MPC_LDS_BASE_MODES >> tm) & 1);
+}
 template <int WIN> constexpr int stage_bufs() { return parse_dma<WIN>() ? 2 : 1; }
 
 template <int WIN, bool SV>              // SV: the read-base slots (lds_base modes)
 struct alignas(16) WaveLds {            // per-wave LDS of K_parse
   int32_t s_val[SV ? kSlots : 0];       // read base: i = s_val + window prefix of advances
-  int32_t s_ts[kSlots];                 // tstart (clamped; -1: negative)
+  int32_t s_ts[kSlots];                 // tstart (clamped to [MPC_TSTART_MIN, kICap])
   int32_t s_read[kSlots];               // local read index
   int32_t s_iend[kSlots];               // i_end | bit 30: read has a downstream flank
   int64_t s_end[kSlots];                // cs offset of the read's end
@@ -891,6 +900,8 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   uint32_t nev = 0;                                       // events written (wave-uniform)
   int64_t rs0 = ra;         // first read whose cs starts at or after P
   bool carry = false;       // slot 0 holds a read continuing into this window
+  bool neg = false;         // a read with a negative tstart reached this chunk: the rounds follow
+                            // Python's negative index wrap (wave-uniform, sticky for the chunk)
   int32_t c_base = 0;       // ... and its coordinate base (wave-uniform): i = base + window prefix of advances
   constexpr bool dma = parse_dma<WIN>();
   int sb = 0;               // stage buffer of the current window
@@ -992,19 +1003,23 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     }
     const bool inwin = l < 63 && cur.o < C;  // read rs0+l starts in [P, C)
     const int nst = __popcll(ballot(inwin));
+    neg = neg || ballot(inwin && cur.ts < 0) != 0;
     // ---- per-read slots ----
     if (inwin) {
       const int q = l + 1;
       const bool up = uo_nx != cur.uo, dn = dno_nx != cur.dno;  // flank lengths < 2^32
       const int ts = cur.ts;
       uint32_t derr = 0;
-      if (ts < 0) derr |= DE_INDEX;                   // deviation: no negative wrap
+      // obsarr[2 tstart] (:303) with Python's negative wrap: below -n past the
+      // front (IndexError), in [-n, 0) a wrapped ODD position (not supported)
+      if (up && ts < 0) derr |= ts + n >= 0 ? DE_UNSUP : DE_INDEX;
+      if (ts < MPC_TSTART_MIN) derr |= DE_UNSUP;
       if (up && ts > n) derr |= DE_INDEX;             // leftIndel(2*i) past the end
       if (o_nx <= cur.o) derr |= DE_OP;               // processOperation('', '')
       if (derr) flag_read(a, derr, rs0 + l);
       if (up && ts >= 0 && ts <= n) left_bit(ts);  // upstream flank: LEFT at gap tstart
       W.s_end[q] = o_nx;
-      W.s_ts[q] = ts < 0 ? -1 : (ts > kICap ? kICap : ts);
+      W.s_ts[q] = ts < MPC_TSTART_MIN ? MPC_TSTART_MIN : (ts > kICap ? kICap : ts);
       W.s_read[q] = (int32_t)(rs0 + l);
       W.s_iend[q] = (ts < 0 ? 0 : (ts > n ? n + 1 : ts)) | (dn ? 1 << 30 : 0);
     }
@@ -1137,11 +1152,17 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         const uint32_t vm = ol4 == 4 ? 0xffffffffu : ((1u << (8 * ol4)) - 1u);
         uint32_t pk = (codes | (codes >> 6)) & 0x000f000fu;
         pk = (pk | (pk >> 12)) & ((1u << (2 * ol4)) - 1u);
-        fast = !v | (!lfar & (olen >= 1) & (olen <= 4) & dig &
-                     (colon | minus | (star & (((bad >> shl) & 0xffu) == 0u)) | (plus & ((bad & vm) == 0u))));
+        // a special token with an empty operand that is not its read's last --
+        // the 'Z' and ':' every read's cs starts with ("Z::12*ag") -- is a no-op
+        // (:309: the operator is only applied to a non-empty operand); no prefix
+        // can precede it ('Z' / ':' / '*' / '+' / '-' are never absorbed digits)
+        const bool nop = (olen == 0) & !last & (pl == 0) & (colon | star | plus | minus | (op == 'Z'));
+        fast = !v | (!lfar & ((olen >= 1) & (olen <= 4) & dig &
+                              (colon | minus | (star & (((bad >> shl) & 0xffu) == 0u)) | (plus & ((bad & vm) == 0u))) |
+                              nop));
         // branch-free: '*' 0x2A -> 2, '+' 0x2B -> 3, '-' 0x2D -> 4 from op & 7;
-        // ':' -> 1 when it matches at least one base (:77)
-        const int mv = -(int)v, mc = -(int)colon;
+        // ':' -> 1 when it matches at least one base (:77); a no-op: 0
+        const int mv = -(int)(v & !nop), mc = -(int)colon;
         const int o7 = (int)(op & 7u);
         kind = mv & ((mc & (int)(val > 0)) | (~mc & (o7 - (o7 >> 2))));
         adv = mv & ((mc & val) | (int)star | (-(int)minus & ol4));
@@ -1227,7 +1248,16 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       // scalar pass over the start lanes (about one per round: reads hold tens
       // to hundreds of units) instead of an LDS write, fence and read back
       int bv = cb;
-      if constexpr (lds_base<TM>()) {
+      if constexpr (bperm_base<TM>()) {
+        // the last read start at or below this lane (its base by one
+        // ds_bpermute), else the read open since an earlier round (cb)
+        const uint64_t le = brs & (~0ull >> (63 - l));
+        const int mine = q_ts - (G + aex);
+        const int ls = le ? 63 - __clzll((long long)le) : 0;
+        const int sv = __builtin_amdgcn_ds_bpermute(ls << 2, mine);
+        bv = le ? sv : cb;
+        if (brs) cb = __builtin_amdgcn_readlane(mine, 63 - __clzll((long long)brs));
+      } else if constexpr (lds_base<TM>()) {
         if (is_rs) W.s_val[q] = q_ts - (G + aex);
         wave_sync_lds();
         const int sv = W.s_val[q];
@@ -1247,20 +1277,38 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       // IndexError (refarr / obsarr past the end): a ':' prefix writes [iu, i),
       // ':' [i, i + adv), '*' [i, i + 1), '+' the gap i: every kind 1-3 needs
       // 0 <= i and i + adv <= n (adv = 1 for '*', 0 for '+'); sign of an OR
-      const bool bad_i = ((adv0 > 0) & ((iu | (n - i)) < 0)) | (((uint32_t)(kind - 1) <= 2u) & ((i | (n - adv - i)) < 0));
-      uint32_t te = err | (bad_i ? DE_INDEX : 0u);
+      bool bad_i = ((adv0 > 0) & ((iu | (n - i)) < 0)) | (((uint32_t)(kind - 1) <= 2u) & ((i | (n - adv - i)) < 0));
+      // Negative coordinates (a negative tstart; chunks that hold one only):
+      // refarr / obsarr take index x at len + x for x in [-(2n+1), 0)
+      // (Python list indexing).  A ':' or '-' there writes nothing
+      // (the wrapped refarr index is even: ''); a '*' at i < 0 writes its base
+      // as a one-base LEFT string at gap n + 1 + i; a '+' at i in [-n, 0) would
+      // write slots into a wrapped ODD position: unsupported (MPC_DE_UNSUPPORTED)
+      bool wrap = false, unsup = false;
+      int di = i, gi = i, li = olen_e;  // deletion start, LEFT gap and length
+      if (neg) {
+        const bool mat = (kind == 1) | (kind == 2);
+        bad_i = ((adv0 > 0) & (((iu + n + 1) | (n - i)) < 0)) | (mat & (((i + n + 1) | (n - adv - i)) < 0)) |
+                ((kind == 3) & (((i + n) | (n - i)) < 0));
+        unsup = (kind == 3) & (i < 0) & (i + n >= 0);
+        wrap = (kind == 2) & (i < 0);
+        di = i < 0 ? 0 : i;
+        gi = wrap ? i + n + 1 : i;
+        li = wrap ? 1 : olen_e;
+      }
+      uint32_t te = err | (bad_i ? DE_INDEX : 0u) | (unsup ? DE_UNSUP : 0u);
       const int rl = q_read;
       const bool ok = te == 0;
-      if (ok & (kind == 2) & (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
-      const bool del = ok & (kind == 4) & (i >= 0) & (i < n);
+      if (ok & (kind == 2) & !wrap & (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
+      const bool del = ok & (kind == 4) & (di < n) & (i + olen_e > di);
       if (del) {
-        depth_dec(i);
+        depth_dec(di);
         depth_inc(i + olen_e < n ? i + olen_e : n);
       }
-      if (ok & (kind == 3)) left_bit(i);
+      if (ok & ((kind == 3) | wrap)) left_bit(gi);
       if (ok & (kind == 3) & (olen_e > kInsInline)) push_ovf(a, A + sx + 1, rl, i, olen_e);
       if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window
-        const bool sev = ok && kind == 2;
+        const bool sev = ok && kind == 2 && !wrap;
         const int win = i >> kSubWinBits;
         uint16_t* wp = a.subev + sev_base;  // window ww's region of this wave
         for (int ww = 0; ww < a.sub_wins; ++ww, wp += a.subev_cap) {
@@ -1272,21 +1320,23 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
           if (l == ww) nsub_v += (uint32_t)__popcll(bw);
         }
       }
-      const bool ins_inline = kind == 3 && olen_e <= kInsInline && ok;
+      const bool ins_inline = ((kind == 3 && olen_e <= kInsInline) || wrap) && ok;
       const uint64_t bins = ballot(ins_inline);
       if (ins_inline) {
-        a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(i, olen_e, pay, a.read_offset + rl);
-        bucket_add(i);
+        a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(gi, li, pay, a.read_offset + rl);
+        bucket_add(gi);
       }
       if (last) {  // the read's last operation: i_end, downstream check, span
         const int ia = i + adv;
         const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
         const int dnf = q_iend & (1 << 30);
         if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
+        // ... or, wrapped, past the front / into an odd position (unsupported)
+        if (neg && dnf && ia < 0) te |= ia + n >= 0 ? DE_UNSUP : DE_INDEX;
         W.s_iend[q] = ie | dnf;
-        const int ts = q_ts;
+        const int ts = q_ts < 0 ? 0 : q_ts;  // matches below 0 write nothing
         const int e2 = ie > n ? n : ie;
-        if (ts >= 0 && ts < e2) { depth_inc(ts); depth_dec(e2); }
+        if (ts < e2) { depth_inc(ts); depth_dec(e2); }
       }
       if (te) flag_read(a, te, rl);
       G += atot;

@@ -16,13 +16,14 @@ LIB_PATH = _build.LIBMPC
 
 ABI_VERSION = 7
 MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED = 0, 1, 2, 3
-DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL = 1, 2, 4, 8, 16, 32
+DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL, DE_UNSUPPORTED = 1, 2, 4, 8, 16, 32, 64
 (BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_CNT, BUF_RIGHT_CNT_ALL,
  BUF_HASLEFT, BUF_MAXR, BUF_RUN_M, BUF_RUN_R, BUF_DIFF, BUF_SUB) = range(14)
 PHASES = ("parse", "index", "runs", "tally", "layout", "rows")
 
 DE_NAMES = {DE_OP: "Unknown operator", DE_VALUE: "ValueError", DE_INDEX: "IndexError", DE_KEY: "KeyError",
-            DE_CAPACITY: "row capacity", DE_INTERNAL: "internal invariant"}
+            DE_CAPACITY: "row capacity", DE_INTERNAL: "internal invariant",
+            DE_UNSUPPORTED: "unsupported input (a negative target start writing into a wrapped odd position)"}
 K_PARSE, K_ODD, K_LEFT, K_FLANK, K_INS, K_RSORT = 0, 1, 2, 3, 4, 5
 CS_PAD = 2048  # readable bytes required past the end of the cs buffer (mpc.h)
 FLANK_PAD = 16  # readable bytes required past the end of the up/down buffers (mpc.h)

@@ -25,6 +25,8 @@ import os
 import numpy as np
 
 BASE_COMPLIMENT = {"A": "T", "T": "A", "G": "C", "C": "G", "N": "N"}  # :27
+# lowest target start the device takes (mpc.h MPC_TSTART_MIN: -2^28)
+TSTART_MIN = -(1 << 28)
 _RC_TABLE = str.maketrans("ACGTN", "TGCAN")
 _ALLOWED_RC = frozenset("ACGTN")
 
@@ -392,7 +394,7 @@ def pack_sample_python(ref_path, paf_path, reads_path):
         fl = flanks.get(name)
         if fl is None:  # paf[read_name]["upstream_seq"] -> KeyError (:303)
             raise IngestError(f"KeyError: 'upstream_seq' (read {name} not in {reads_path})")
-        if t < 0 or t >= 2 ** 31:
+        if t < TSTART_MIN or t >= 2 ** 31:  # (negative starts: the device wraps them like Python, mpc.h)
             raise IngestError(f"target start {t} of read {name} out of range (unsupported)")
         cs.append(transcode_cs(c))
         up.append(transcode_flank(fl[0]))

@@ -27,8 +27,12 @@
  *   ORC_E_INDEX  IndexError (position past the reference; :57/:69/:79, '*' with empty operand :96)
  *   ORC_E_VALUE  ValueError (int() of a ':' operand; :77)
  *   ORC_E_OP     sys.exit("Unknown operator") (:100-102)
- * Deviation shared with the HIP path: a negative target start is rejected
- * (ORC_E_INDEX) instead of wrapping with Python negative indexing.
+ * Indices follow Python's list semantics exactly, negative wrap included
+ * (obs_index): a negative target start (never written by minimap2) reaches
+ * refarr / obsarr at len + index, like the reference (:222, :300-303, :57-61,
+ * :69, :79, :87, :96), pinned by tests/golden/n_neg_*.  The HIP path
+ * implements the part of it that keeps odd positions single-slot and rejects
+ * the rest (MPC_DE_UNSUPPORTED, include/mpc.h).
  */
 #include <stdint.h>
 #include <stdlib.h>
@@ -70,10 +74,17 @@ static int grow(Pos* p) {
   return 0;
 }
 
+/* Python list index: x in [-P, P) -> x mod P, else -1 (IndexError) */
+static int64_t obs_index(int64_t x, int64_t P) {
+  if (x < 0) x += P;
+  return (x < 0 || x >= P) ? -1 : x;
+}
+
 /* processBaseString_leftIndel (:37-62) */
-static int left_indel(Pos* obs, int64_t P, int64_t x, const char* str, int64_t L, int upper) {
+static int left_indel(Pos* obs, int64_t P, int64_t x0, const char* str, int64_t L, int upper) {
+  const int64_t x = obs_index(x0, P);
   for (int64_t bi = 0; bi < L; ++bi) {
-    if (x < 0 || x >= P) return ORC_E_INDEX;
+    if (x < 0) return ORC_E_INDEX;
     char b = str[L - bi - 1];
     if (upper) b = upc(b);
     Pos* p = &obs[x];
@@ -91,9 +102,10 @@ static int left_indel(Pos* obs, int64_t P, int64_t x, const char* str, int64_t L
 }
 
 /* processBaseString_rightIndel (:64-72) */
-static int right_indel(Pos* obs, int64_t P, int64_t x, const char* str, int64_t L) {
+static int right_indel(Pos* obs, int64_t P, int64_t x0, const char* str, int64_t L) {
+  const int64_t x = obs_index(x0, P);
   for (int64_t bi = 0; bi < L; ++bi) {
-    if (x < 0 || x >= P) return ORC_E_INDEX;
+    if (x < 0) return ORC_E_INDEX;
     char b = str[bi];
     Pos* p = &obs[x];
     if (p->len <= bi) {
@@ -141,16 +153,21 @@ static int py_int(const char* s, int64_t len, int64_t* out) {
 }
 
 /* processOperation (:74-104); i is the reference coordinate, updated in place */
-static int process_op(Pos* obs, int64_t P, const char* ref, int64_t n, int64_t* i, char op,
+static int process_op(Pos* obs, int64_t P, const char* ref, int64_t* i, char op,
                       const char* operand, int64_t olen) {
   if (op == ':') {
     int64_t v;
     int e = py_int(operand, olen, &v);
     if (e) return e;
     for (int64_t x = 0; x < v; ++x) {
-      if (*i < 0 || *i >= n) return ORC_E_INDEX; /* refarr[(2*i)+1] */
-      e = left_indel(obs, P, 2 * (*i) + 1, ref + *i, 1, 0);
-      if (e) return e;
+      /* refarr[(2*i)+1]: an odd index holds ref[i], an even one (reached by a
+       * wrapped negative index) holds '' */
+      const int64_t ri = obs_index(2 * (*i) + 1, P);
+      if (ri < 0) return ORC_E_INDEX;
+      if (ri & 1) {
+        e = left_indel(obs, P, ri, ref + (ri - 1) / 2, 1, 0);
+        if (e) return e;
+      }
       *i += 1;
     }
   } else if (op == '+') {
@@ -173,14 +190,13 @@ static int process_op(Pos* obs, int64_t P, const char* ref, int64_t n, int64_t* 
 static int is_special(char c) { return c == ':' || c == 'Z' || c == '+' || c == '-' || c == '*'; }
 
 /* Step 4 (:285-323) for all reads. */
-static int oracle_pileup(Pos* obs, int64_t P, const char* ref, int64_t n, int64_t nreads,
+static int oracle_pileup(Pos* obs, int64_t P, const char* ref, int64_t nreads,
                          const char* cs, const int64_t* cs_off, const int64_t* tstart,
                          const char* up, const int64_t* up_off, const char* down,
                          const int64_t* down_off, int64_t* err_read) {
   for (int64_t r = 0; r < nreads; ++r) {
     int64_t i = tstart[r];
     *err_read = r;
-    if (i < 0) return ORC_E_INDEX;
     int e = left_indel(obs, P, 2 * i, up + up_off[r], up_off[r + 1] - up_off[r], 0);
     if (e) return e;
     const char* c = cs + cs_off[r];
@@ -190,7 +206,7 @@ static int oracle_pileup(Pos* obs, int64_t P, const char* ref, int64_t n, int64_
     for (int64_t k = 0; k < len; ++k) {
       if (is_special(c[k])) {
         if (olen != 0) {
-          e = process_op(obs, P, ref, n, &i, op, c + ostart, olen);
+          e = process_op(obs, P, ref, &i, op, c + ostart, olen);
           if (e) return e;
         }
         op = c[k];
@@ -200,7 +216,7 @@ static int oracle_pileup(Pos* obs, int64_t P, const char* ref, int64_t n, int64_
         olen += 1;
       }
     }
-    e = process_op(obs, P, ref, n, &i, op, c + ostart, olen);
+    e = process_op(obs, P, ref, &i, op, c + ostart, olen);
     if (e) return e;
     e = right_indel(obs, P, 2 * i, down + down_off[r], down_off[r + 1] - down_off[r]);
     if (e) return e;
@@ -288,7 +304,7 @@ int mpc_oracle_run(const char* ref, int64_t n, int64_t nreads, const char* cs, c
   Pos* obs = (Pos*)calloc((size_t)P, sizeof(Pos));
   if (!obs) { out->err = ORC_E_NOMEM; return out->err; }
   int64_t er = -1;
-  int e = oracle_pileup(obs, P, ref, n, nreads, cs, cs_off, tstart, up, up_off, down, down_off, &er);
+  int e = oracle_pileup(obs, P, ref, nreads, cs, cs_off, tstart, up, up_off, down, down_off, &er);
   if (e) { out->err = e; out->err_read = er; }
   else { e = oracle_consensus(obs, P, mdf, gtf, out); out->err = e; }
   for (int64_t x = 0; x < P; ++x) free(obs[x].s);

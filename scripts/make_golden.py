@@ -248,17 +248,54 @@ def random_cases(script):
                       open(p("as.paf"), "rb").read(), sweep[:3], "same reads vs revcomp reference")
 
 
+def negative_cases(script):
+    """PAF target starts below 0 (minimap2 never writes one; the reference then
+    indexes refarr / obsarr with Python's negative wrap, :222, :300-303,
+    :57-61, :79, :87, :96).  Pins what the reference does: a match or deletion
+    at a negative coordinate >= -(n+1) is a no-op (the wrapped refarr index is
+    even, i.e. ''), a '*' writes a one-base LEFT string at the wrapped even
+    index, a '+' / flank writes slots into a wrapped ODD position."""
+    R = ">ref\nACGTACGTAC\n"
+    ok = paf_line("r1", 10, 0, 10, "+", 0, 10, ":10")
+    two = ">r1\nACGTACGTAC\n>r2\nACGTACGTAC\n"
+    emit_case(script, "n_neg_match", R, two, ok + paf_line("r2", 10, 0, 10, "+", -3, 7, ":10"),
+              [(0, 1), (-1, 1)], "negative tstart, matches only: the ones below 0 are no-ops")
+    emit_case(script, "n_neg_del", R, ">r1\nACGTACGTAC\n>r2\nACGTACGT\n",
+              ok + paf_line("r2", 8, 0, 8, "+", -2, 8, "-ac:8"), [(0, 1), (-1, 1)],
+              "negative tstart, a deletion crossing 0")
+    emit_case(script, "n_neg_far_del", R, ">r1\nACGTACGTAC\n>r2\nACGTA\n",
+              ok + paf_line("r2", 5, 0, 5, "+", -15, 5, "-" + "a" * 15 + ":5"), [(0, 1)],
+              "negative tstart below -(n+1), deletion only: no index is taken")
+    emit_case(script, "n_neg_far_match", R, two, ok + paf_line("r2", 10, 0, 10, "+", -12, 8, ":20"), [(0, 1)],
+              "a match below -(n+1): IndexError")
+    emit_case(script, "n_neg_sub", R, two, ok + paf_line("r2", 10, 0, 10, "+", -2, 8, "*ag:9"), [(0, 1), (-1, 1)],
+              "'*' at a negative coordinate: a one-base LEFT string at the wrapped even index")
+    emit_case(script, "n_neg_ins", R, ">r1\nACGTACGTAC\n>r2\nAAACGTACGTAC\n",
+              ok + paf_line("r2", 12, 0, 12, "+", -1, 9, "+aa:10"), [(0, 1), (-1, 1)],
+              "'+' at a negative coordinate: slots in a wrapped odd position")
+    emit_case(script, "n_neg_flank", R, ">r1\nACGTACGTAC\n>r2\nGGACGTACGT\n",
+              ok + paf_line("r2", 10, 2, 10, "+", -2, 6, ":8"), [(0, 1), (-1, 1)],
+              "upstream flank at a negative tstart: slots in a wrapped odd position")
+    emit_case(script, "n_neg_end", R, ">r1\nACGTACGTAC\n>r2\nACGTT\n",
+              ok + paf_line("r2", 5, 0, 3, "+", -8, -5, ":3"), [(0, 1), (-1, 1)],
+              "a read ending below 0 with a downstream flank: slots appended to a wrapped odd position")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref-script", default="/root/reference/src/mapped_paf_read_parser.py")
-    ap.add_argument("--only", default="", help="'unicode': regenerate only the non-ASCII cases")
+    ap.add_argument("--only", default="", help="'unicode' / 'negative': regenerate only the non-ASCII / negative-tstart cases")
     a = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
     if a.only == "unicode":
         unicode_cases(a.ref_script)
         return
+    if a.only == "negative":
+        negative_cases(a.ref_script)
+        return
     hand_cases(a.ref_script)
     unicode_cases(a.ref_script)
+    negative_cases(a.ref_script)
     random_cases(a.ref_script)
 
 

@@ -76,6 +76,8 @@ extern "C" {
 #define MPC_ST_ROWS_NEEDED 2 /* rows (pileup slots incl. empty odd positions) the layout needs */
 #define MPC_ST_MIXED 3       /* downstream (RIGHT) events at gaps that also hold LEFT events */
 #define MPC_ST_UNITS 4       /* internal: work units of the bucketed event tallies */
+#define MPC_ST_RSORT_PATH 5  /* internal: sort of the mixed RIGHT events -- 0 one workgroup (planned), 1 the
+                               multi-workgroup path ran, 2 it was planned but fell back to one workgroup */
 #define MPC_ST_WORDS 8
 
 /* Per-read inputs, already in HBM.  One sample = one (assembly, PAF) pair, e.g.

@@ -290,19 +290,22 @@ struct NameTable {
         slot[i].store(~(uint64_t)0, std::memory_order_relaxed);
     });
   }
-  // name_of(index) -> the name of a record already inserted
+  // name_of(index) -> the name of a record already inserted.  A slot value is
+  // published with release and read with acquire, so the record it names
+  // (written by the publishing thread before the insert) is visible to a
+  // thread that compares names through it.
   template <class NameOf>
   void insert(uint32_t idx, sv name, uint64_t h, NameOf name_of) {
     const uint64_t v = (h >> 32) << 32 | idx;
     for (uint64_t p = h & mask;; p = (p + 1) & mask) {
-      uint64_t cur = slot[p].load(std::memory_order_relaxed);
+      uint64_t cur = slot[p].load(std::memory_order_acquire);
       for (;;) {
         if (cur == ~(uint64_t)0) {
-          if (slot[p].compare_exchange_weak(cur, v, std::memory_order_relaxed)) return;
+          if (slot[p].compare_exchange_weak(cur, v, std::memory_order_acq_rel, std::memory_order_acquire)) return;
           continue;  // cur reloaded
         }
         if ((cur >> 32) != (v >> 32) || name_of((uint32_t)cur) != name) break;  // another name: probe on
-        while (v < cur && !slot[p].compare_exchange_weak(cur, v, std::memory_order_relaxed)) {}
+        while (v < cur && !slot[p].compare_exchange_weak(cur, v, std::memory_order_acq_rel, std::memory_order_acquire)) {}
         return;
       }
     }
@@ -312,7 +315,7 @@ struct NameTable {
   uint64_t find(sv name, NameOf name_of) const {
     const uint64_t h = hash(name);
     for (uint64_t p = h & mask;; p = (p + 1) & mask) {
-      const uint64_t cur = slot[p].load(std::memory_order_relaxed);
+      const uint64_t cur = slot[p].load(std::memory_order_acquire);
       if (cur == ~(uint64_t)0) return cur;
       if ((cur >> 32) == (h >> 32) && name_of((uint32_t)cur) == name) return cur;
     }

@@ -67,13 +67,20 @@ constexpr uint32_t DE_OP = MPC_DE_OP, DE_VALUE = MPC_DE_VALUE, DE_INDEX = MPC_DE
 constexpr int kBlk = 1024;          // cs bytes staged per wave iteration (64 lanes x 16 B)
 constexpr int kInsInline = 4;       // insertions up to this length travel as one event word
 // 32-bit coordinates: a unit's advances are clamped at kAdvCap > n (a clamped
-// advance still leaves i past the end); a window's prefix of advances then
-// stays below (WIN / 8) * 2^23 (a ':' operand worth 2^22 takes >= 8 bytes) and
-// every coordinate below kICap + 2^30 + 2^29 < 2^31.  The insertion event word
+// advance still leaves i past the end).  An advance of 2^22 takes at least 8 cs
+// bytes (':' + 7 digits; a '-' advances by its operand bytes), so a window's
+// prefix of advances stays below (WIN / 8) * 2^22 <= 2^30 at the largest
+// window, and a coordinate (a read base <= kICap plus that prefix plus one
+// unit's advance) below 2^31 (static_assert below).  The insertion event word
 // holds the gap in 22 bits (kNullGap).
 constexpr int kMaxRefLen = (1 << 22) - 2;
 constexpr int kAdvCap = 1 << 22;    // > any reference length: a clamped advance keeps i past the end
 constexpr int kICap = 1 << 28;      // saturation of the running coordinate i
+constexpr int kMaxWin = 2048;       // largest parse window (bytes)
+static_assert((int64_t)kICap + (int64_t)(kMaxWin / 8) * kAdvCap + 2 * (int64_t)kAdvCap < (int64_t)INT32_MAX,
+              "32-bit coordinates: read base + window prefix of advances + one unit");
+static_assert((int64_t)MPC_TSTART_MIN - (int64_t)(kMaxWin / 8) * kAdvCap > (int64_t)INT32_MIN,
+              "32-bit coordinates below 0 (negative target starts)");
 constexpr int kBW = 64;             // gaps per insertion bucket (K_left workgroup)
 static_assert(kBW <= 64 && (kBW & (kBW - 1)) == 0, "sorted insertion events hold the gap within its bucket in 6 bits");
 constexpr int kKMax = 8;            // runs per gap tallied in K_left's LDS (others go to HBM)
@@ -804,6 +811,7 @@ __device__ void parse_epilogue_big(const ParseArgs& a, int n, int nbk, int64_t r
 template <int TM, int WIN>
 __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   constexpr int CH = WIN / 64;
+  static_assert(WIN <= kMaxWin, "coordinate bound (kMaxWin)");
   using WL = WaveLds<WIN, lds_base<TM>()>;
   extern __shared__ __attribute__((aligned(16))) uint8_t lds[];
   const int l = lane();
@@ -1952,6 +1960,7 @@ __global__ __launch_bounds__(1024) void K_rscan2(Dev d, int32_t nblk_scan) {
   if (blockIdx.x == 0 && tid == 0) {
     const bool multi = s_tot > kSortLds && s_max <= kSegMax;
     d.rsflag[0] = multi ? 1 : 0;
+    d.status[MPC_ST_RSORT_PATH] = multi ? 1u : 2u;
     if (multi) d.status[MPC_ST_MIXED] = (uint32_t)s_tot;
   }
 }

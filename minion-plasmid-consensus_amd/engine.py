@@ -15,7 +15,7 @@ from . import _build
 LIB_PATH = _build.LIBMPC
 
 ABI_VERSION = 7
-MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED = 0, 1, 2, 3
+MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED, MPC_ST_RSORT_PATH = 0, 1, 2, 3, 5
 DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL, DE_UNSUPPORTED = 1, 2, 4, 8, 16, 32, 64
 (BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_CNT, BUF_RIGHT_CNT_ALL,
  BUF_HASLEFT, BUF_MAXR, BUF_RUN_M, BUF_RUN_R, BUF_DIFF, BUF_SUB) = range(14)
@@ -96,22 +96,70 @@ def _hip_runtime_paths():
     return paths
 
 
-def _preload_hip_runtime():
-    """libmpc.so needs libamdhip64.so.7 (its SONAME).  PyTorch-ROCm ships its own
-    copy of that library (same SONAME) with its own HSA runtime in torch/lib;
-    two HIP/HSA runtimes in one process leave the second one with "no
-    ROCm-capable device".  When PyTorch is installed, map ITS copy first
-    (RTLD_GLOBAL, by path, without importing torch): the dynamic linker then
-    binds libmpc.so's dependency to it by SONAME, and a later ``import torch``
-    finds the same file already mapped -- one runtime in either import order.
-    Without PyTorch (a C-ABI user) the system ROCm copy is used."""
+def _elf_dynamic(path):
+    """(SONAME, [NEEDED...]) of an ELF64 little-endian shared library, from its
+    .dynamic section (no tools, no loading); (None, []) if unreadable."""
+    import struct
+    try:
+        with open(path, "rb") as f:
+            data = f.read()
+        if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
+            return None, []
+        shoff, = struct.unpack_from("<Q", data, 0x28)
+        shentsize, shnum = struct.unpack_from("<HH", data, 0x3A)
+        secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + k * shentsize) for k in range(shnum)]
+        dyn = next((sh for sh in secs if sh[1] == 6), None)  # SHT_DYNAMIC
+        if dyn is None:
+            return None, []
+        strtab = secs[dyn[6]]  # sh_link: its string table
+        sname = lambda o: data[strtab[4] + o: data.index(b"\0", strtab[4] + o)].decode()
+        soname, needed = None, []
+        for k in range(dyn[5] // 16):
+            tag, val = struct.unpack_from("<qQ", data, dyn[4] + 16 * k)
+            if tag == 0:
+                break
+            if tag == 14:
+                soname = sname(val)
+            elif tag == 1:
+                needed.append(sname(val))
+        return soname, needed
+    except (OSError, ValueError, struct.error, IndexError, StopIteration, UnicodeDecodeError):
+        return None, []
+
+
+def _torch_hip_runtime():
+    """Path of PyTorch's own libamdhip64.so (torch/lib), without importing torch."""
     import importlib.util
     spec = importlib.util.find_spec("torch")
     if spec is None or not spec.origin:
-        return
+        return None
     path = os.path.join(os.path.dirname(spec.origin), "lib", "libamdhip64.so")
-    if os.path.exists(path):
-        ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    return path if os.path.exists(path) else None
+
+
+def _preload_hip_runtime():
+    """libmpc.so needs libamdhip64.so.N (NEEDED).  PyTorch-ROCm ships its own
+    copy of that library with its own HSA runtime in torch/lib; two HIP/HSA
+    runtimes in one process leave the second one with "no ROCm-capable
+    device".  When PyTorch's copy has the SONAME libmpc.so needs, map it first
+    (RTLD_GLOBAL, by path, without importing torch): the dynamic linker then
+    binds libmpc.so's dependency to it by SONAME, and a later ``import torch``
+    finds the same file already mapped -- one runtime in either import order.
+    When the SONAMEs differ (a PyTorch built against another HIP major) the
+    two cannot be shared: initialise PyTorch first so that its runtime is the
+    one in use, and report both names if a second runtime gets mapped anyway.
+    Without PyTorch (a C-ABI user) the system ROCm copy is used.  Returns
+    (torch's SONAME, libmpc's NEEDED HIP runtime) for the error message."""
+    path = _torch_hip_runtime()
+    if path is None:
+        return None, None
+    torch_so, _ = _elf_dynamic(path)
+    need = next((x for x in _elf_dynamic(LIB_PATH)[1] if x.startswith("libamdhip64.so")), None)
+    if torch_so is not None and need is not None and torch_so != need:
+        _torch().cuda.is_available()  # PyTorch's runtime first (the pre-round-4 order)
+        return torch_so, need
+    ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
+    return torch_so, need
 
 
 def lib():
@@ -119,10 +167,13 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise MpcError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() (no CPU fallback)")
-        _preload_hip_runtime()
+        torch_so, need = _preload_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)
         rt = _hip_runtime_paths()
         if len(rt) > 1:
+            if torch_so != need:
+                raise MpcError("libmpc.so needs %s but PyTorch ships %s: two HIP runtimes are mapped (%s); "
+                               "rebuild libmpc.so against PyTorch's HIP" % (need, torch_so, ", ".join(sorted(rt))))
             raise MpcError("two HIP runtimes are mapped into this process (%s): load libmpc.so through "
                            "engine.lib() before anything else loads a HIP runtime" % ", ".join(sorted(rt)))
         vp, i64, i32, dbl = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double

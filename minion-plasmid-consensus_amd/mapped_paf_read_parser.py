@@ -104,17 +104,30 @@ def _ingest_and_pileup(ingest, engine, jobs, args, tm):
         if mdf is None:
             return None
         results = [None] * len(jobs)
-        read0 = 0
+        # reads of every job, and the job-order prefix: a device error is
+        # reported as the read index in the launch of all jobs in JOB order
+        n_of = [len(packed[j]["tstart"]) for j in range(len(jobs))]
+        before = [sum(n_of[:j]) for j in range(len(jobs))]
+        first = None  # (job, read within it, flags) of the earliest failing job
         for idx, f in futs:
             try:
                 res = f.result()
-            except engine.DataError as e:  # read index in the launch of all jobs, as before
-                for _, g in futs:
-                    g.exception()
-                raise engine.DataError(e.flags, e.read + read0)
+            except engine.DataError as e:
+                # the group's samples are its jobs in idx order: map the launch's
+                # read index back to (job, read in the job)
+                r = e.read
+                for k, j in enumerate(idx):
+                    if r < n_of[j] or k == len(idx) - 1:
+                        break
+                    r -= n_of[j]
+                if first is None or j < first[0]:
+                    first = (j, r, e.flags)
+                continue
             for j, r in zip(idx, res):
                 results[j] = r
-            read0 += sum(len(packed[j]["tstart"]) for j in idx)
+        if first is not None:
+            j, r, flags = first
+            raise engine.DataError(flags, before[j] + r)
     tm["device"] = time.perf_counter() - t1
     return results
 

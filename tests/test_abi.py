@@ -217,3 +217,29 @@ def test_product_build_flags(pkg):
     assert lib.mpc_build_flags() == 0
     src = open(os.path.join(REPO, "minion-plasmid-consensus_amd", "csrc", "mpc_kernels.hip")).read()
     assert "MPC_ABL_" not in src and "wrong results" not in src
+
+
+def test_hip_runtime_soname_check(pkg, monkeypatch):
+    """the torch-first preload compares SONAMEs.  Same SONAME ->
+    map PyTorch's copy by path; a different one (PyTorch on another HIP major)
+    -> initialise PyTorch first instead, and name both in the error."""
+    e = pkg.engine
+    need = [x for x in e._elf_dynamic(e.LIB_PATH)[1] if x.startswith("libamdhip64.so")]
+    assert len(need) == 1
+    tpath = e._torch_hip_runtime()
+    if tpath is not None:
+        assert e._elf_dynamic(tpath)[0].startswith("libamdhip64.so")
+    seen = []
+    monkeypatch.setattr(e, "_torch_hip_runtime", lambda: "/x/libamdhip64.so")
+    monkeypatch.setattr(e, "_elf_dynamic", lambda p: ("libamdhip64.so.9", []) if p.startswith("/x/")
+                        else (None, ["libamdhip64.so.7"]))
+
+    class T:
+        class cuda:
+            @staticmethod
+            def is_available():
+                seen.append("torch first")
+                return False
+    monkeypatch.setattr(e, "_torch", lambda: T)
+    assert e._preload_hip_runtime() == ("libamdhip64.so.9", "libamdhip64.so.7")
+    assert seen == ["torch first"]

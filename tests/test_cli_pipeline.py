@@ -36,8 +36,11 @@ def launches(monkeypatch):
 
     def fake_pileup(samples, mdf, gtf, device=0, row_cap=None):
         calls.append([len(s["tstart"]) for s in samples])
+        fail = getattr(fake_pileup, "fail", {})  # launch number -> failing read index in the launch
         if getattr(fake_pileup, "fail_at", None) == len(calls):
             raise pkg.engine.DataError(pkg.engine.DE_KEY, 1)
+        if len(calls) in fail:
+            raise pkg.engine.DataError(pkg.engine.DE_KEY, fail[len(calls)])
         return [dict(count=[], max_depth=0) for _ in samples]
 
     monkeypatch.setattr(pkg.engine, "pileup", fake_pileup)
@@ -72,3 +75,31 @@ def test_missing_min_depth_factor_after_reading_everything(tmp_path, launches, c
     assert "KeyError" in capsys.readouterr().err and calls == []
     assert cli.main(_argv([a], mdf=None)) == 1
     assert "min_depth_factor is required" in capsys.readouterr().err and calls == []
+
+
+def _interleaved(tmp_path):
+    """jobs A (r1.fa, 2 reads), B (r2.fa, 1 read), C (r1.fa, 1 read): the
+    launches are [A, C] then [B] (one per reads file), not job order."""
+    a = _job(tmp_path, "a", "r1.fa", ["x", "y"], ">x\nACGTACGTAC\n>y\nACGTACGTAC\n>w\nACGTACGTAC\n")
+    b = _job(tmp_path, "b", "r2.fa", ["z"], ">z\nACGTACGTAC\n")
+    c = _job(tmp_path, "c", "r1.fa", ["w"])
+    return [a, b, c]
+
+
+def test_device_error_interleaved_jobs_job_order_index(tmp_path, launches, capsys):
+    """A device error in job C (read 2 of the launch [A, C]) is reported at
+    C's index in JOB order: len(A) + len(B) + 0 = 3."""
+    calls, fake = launches
+    fake.fail = {1: 2}
+    assert cli.main(_argv(_interleaved(tmp_path))) == 1
+    assert calls == [[2, 1], [1]]
+    assert "read index 3" in capsys.readouterr().err
+
+
+def test_device_error_earliest_job_wins(tmp_path, launches, capsys):
+    """Errors in job C (launch 1) and job B (launch 2): B comes first in job
+    order, so its read is reported (index len(A) + 0 = 2)."""
+    calls, fake = launches
+    fake.fail = {1: 2, 2: 0}
+    assert cli.main(_argv(_interleaved(tmp_path))) == 1
+    assert "read index 2" in capsys.readouterr().err

@@ -323,6 +323,37 @@ def test_long_reference_mode4_many_reads(pkg):
             _cmp(got, first, ("mode4_repeat", rep))
 
 
+@pytest.mark.timeout(300)
+def test_max_reference_dense_windows(pkg):
+    """the 32-bit coordinate bound at the largest reference
+    (2^22 - 2 bases, tally mode 4) with parse windows packed with
+    maximal advances -- 63 reads per window of "Z::4194302" (the window
+    prefix of advances reaches ~63 x 2^22), long deletions, a substitution
+    and a negative start -- bit-exact full pileup vs the oracle."""
+    n = (1 << 22) - 2
+    rng = np.random.default_rng(11)
+    ref = np.frombuffer(b"ACGT", np.uint8)[rng.integers(0, 4, n)].copy()
+    cs, ts = [], []
+    for k in range(130):
+        cs.append(b"Z::%d" % n); ts.append(0)
+    for k in range(6):
+        cs.append(b"Z::1000-" + b"a" * 1000 + b":%d" % (n - 2000)); ts.append(0)
+        cs.append(b"Z::2097150*" + b"gat"[k % 3: k % 3 + 1] + b"g" + b":%d" % (n - 2097151)); ts.append(0)
+    cs.append(b"Z::%d" % (n + 5)); ts.append(-5)  # matches below 0 write nothing
+    cs.append(b"Z::%d" % (n - 3)); ts.append(3)
+    off = np.concatenate([[0], np.cumsum([len(c) for c in cs])]).astype(np.int64)
+    z = np.zeros(len(cs) + 1, np.int64)
+    smp = {"ref": ref, "cs": np.frombuffer(b"".join(cs), np.uint8).copy(), "cs_off": off,
+           "tstart": np.array(ts, np.int64), "up": np.zeros(0, np.uint8), "up_off": z, "down": np.zeros(0, np.uint8),
+           "down_off": z.copy()}
+    plan = pkg.engine.Plan(pkg.engine.Batch([smp]))
+    assert plan.info()["tally_mode"] == 4
+    got = pkg.engine.pileup([smp], -1.0, 1.0)[0]
+    exp = _oracle(smp, -1.0, 1.0)
+    assert exp["max_depth"] == 130 + 12 + 2
+    _cmp(got, exp, "max_ref_dense")
+
+
 def test_reference_past_coordinate_limit(pkg):
     """2^22 - 1 bases: beyond the coordinate scheme (mpc.h), rejected."""
     long = {"ref": np.zeros((1 << 22) - 1, dtype=np.uint8) + ord("A"), "cs": np.frombuffer(b"Z::1", np.uint8).copy(),
@@ -352,14 +383,14 @@ def test_mixed_right_sort_paths(pkg, spec, lo, hi):
     _cmp(runner.fetch()[0], _oracle(samples[0], -1.0, 1.0), ("rsort", m))
 
 
-@pytest.mark.parametrize("spec,lo,hi", [
+@pytest.mark.parametrize("spec,lo,hi,path", [
     # more than 512 K_rsplit blocks: the multi-workgroup sort (K_rscan, K_rscatter,
     # K_rsegsort) -- gaps of up to 64 events -- and its fallback to K_rsort
-    # (a gap with more)
-    (dict(n=2000, n_reads=600_000, profile="default", seed=8, frac_partial=0.05), 8193, 600_000),
-    (dict(n=500, n_reads=600_000, profile="indel", seed=9, frac_partial=0.3), 8193, 600_000),
+    # (a gap with more); the path taken is read back (MPC_ST_RSORT_PATH)
+    (dict(n=2000, n_reads=600_000, profile="default", seed=8, frac_partial=0.05), 8193, 600_000, 1),
+    (dict(n=500, n_reads=600_000, profile="indel", seed=9, frac_partial=0.3), 8193, 600_000, 2),
 ], ids=["multi", "multi_fallback"])
-def test_mixed_right_sort_many_reads(pkg, spec, lo, hi):
+def test_mixed_right_sort_many_reads(pkg, spec, lo, hi, path):
     syn = pkg.synth.Synth(antisense=False, **spec)
     samples = [syn.sample(0)]
     runner = pkg.engine.Runner(samples)
@@ -367,6 +398,7 @@ def test_mixed_right_sort_many_reads(pkg, spec, lo, hi):
     runner.check()
     m = int(runner.plan.status()[pkg.engine.MPC_ST_MIXED])
     assert lo <= m <= hi, m
+    assert int(runner.plan.status()[pkg.engine.MPC_ST_RSORT_PATH]) == path
     _cmp(runner.fetch()[0], _oracle(samples[0], -1.0, 1.0), ("rsort many", m))
 
 

@@ -59,7 +59,8 @@ extern "C" {
 #define MPC_DE_UNSUPPORTED 64u /* input the reference accepts but this engine does not: a negative target
                                   start whose upstream flank, '+' insertion or downstream flank Python's
                                   negative index wrap would write into an ODD (reference-base) position
-                                  (tests/golden/n_neg_ins, n_neg_flank, n_neg_end); tstart < MPC_TSTART_MIN */
+                                  (tests/golden/n_neg_ins, n_neg_flank, n_neg_end); a ':' / '-' advance of
+                                  2^22 or more from a negative coordinate; tstart < MPC_TSTART_MIN */
 
 /* Lowest target start the engine takes.  Negative starts (minimap2 never
  * writes one) follow the reference's Python negative indexing (:222,

@@ -30,6 +30,7 @@
 #include <cstring>
 #include <cstdlib>
 #include <string>
+#include <type_traits>
 #include <vector>
 
 #include "mpc.h"
@@ -166,19 +167,27 @@ struct Ovf {  // long insertion (len > kInsInline), tallied by K_flank
   int32_t pad[3];
 };
 
-// insertion event: low word gap<<10 | (len-1)<<8 | bases (2 bits each, string
-// order); high word = global read index
-__device__ __forceinline__ uint64_t ins_event(int gap, int len, uint32_t bases, int64_t rg) {
-  return ((uint64_t)(uint32_t)rg << 32) | ((uint32_t)gap << 10) | ((uint32_t)(len - 1) << 8) | bases;
+// Insertion events (what K_left reads): 4 bytes, bases (8 bits, 2 per base in
+// string order) | (len-1) << 8 | gap within its kBW-gap bucket << 10 | read
+// relative to the parse workgroup's first read << 16 (< 2^15: wg_reads_cap);
+// bit 31 clear.  The bucket and the workgroup are implied by the PAGE the
+// event lies in: K_parse places every event once, into 64-event pages of its
+// (workgroup, bucket), allocated as they fill (parse_place_event); the
+// epilogue lists every bucket's pages, all full but the last (pg_list).
+constexpr int kPgEv = 64;                    // events per page (256 B)
+constexpr int kPgBits = 12;                  // bucket word: page << 12 | fill
+constexpr uint32_t kPgNone = 0xFFFFFu;       // page field of a bucket with no page yet
+constexpr uint32_t kPgInit = (kPgNone << kPgBits) | (uint32_t)kPgEv;  // first event opens a page
+constexpr uint32_t kPgMark = 0xFFFFFFFFu;    // pg_own of a bucket's last page (placed by the epilogue)
+static_assert(kPgEv + 1024 < (1 << kPgBits), "fill field: a full page plus every thread of a block waiting");
+__device__ __forceinline__ uint32_t ins_word(int gap, int len, uint32_t bases, int rel_read) {
+  return bases | ((uint32_t)(len - 1) << 8) | (((uint32_t)gap % (uint32_t)kBW) << 10) | ((uint32_t)rel_read << 16);
 }
-// bucket-sorted insertion event (ins_sorted, what K_left reads): 4 bytes, the
-// bucket and the parse workgroup are implied by the slice it lies in --
-// bases (8 bits) | (len-1) << 8 | gap within the kBW-gap bucket << 10 |
-// read relative to the workgroup's first read << 16 (< 2^15: wg_reads_cap);
-// bit 31 clear (~0u: no event)
-__device__ __forceinline__ uint32_t sorted_event(uint64_t raw, int64_t rg0) {
-  const uint32_t gap = (uint32_t)(raw >> 10) & 0x3fffffu;
-  return ((uint32_t)raw & 0x3ffu) | ((gap % (uint32_t)kBW) << 10) | ((uint32_t)((int64_t)(raw >> 32) - rg0) << 16);
+// page base (in pages) of parse workgroup wg: its events are at most half its
+// cs bytes plus 3 per read (an insertion takes >= 2 cs bytes), i.e. at most
+// bytes / 128 + 3 reads / 64 full pages, plus one partial page per bucket
+__host__ __device__ inline int64_t parse_page_base(int64_t cs_rel, int64_t r, int64_t wg, int nbs) {
+  return cs_rel / 128 + (3 * r) / 64 + wg * (int64_t)(nbs + 4);
 }
 
 struct Dev {  // device-side views of the plan for the small kernels (passed by value)
@@ -364,8 +373,9 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
   const int32_t* wave_tab;  // per workgroup: kMaxCh + 1 read boundaries of its chunks (planner: by cs bytes)
   int64_t cs_base, ovf_cap, read_offset, n_reads;
   int32_t nbs;       // bucket slots per parse workgroup (max buckets)
-  int32_t* i_end; uint64_t* ins_raw; uint32_t* ins_sorted; int32_t* bk_cnt; int32_t* bk_off; int64_t* rbase;
-  int32_t* bk_cur;   // tally mode 4 only: per (workgroup, bucket) scatter cursors
+  int32_t* i_end; uint32_t* ins_sorted; uint32_t* pg_own; uint32_t* pg_list; int32_t* bk_cnt; int32_t* bk_off;
+  int64_t* rbase;
+  uint32_t* bk_cur;  // tally mode 4 only: per (workgroup, bucket) page words in HBM
   Ovf* ovf; uint32_t* ovf_cnt; uint32_t* hasleft; uint32_t* status;
   int32_t* diff; uint32_t* sub;
   // tally mode 3: substitutions as 2-byte events per (wave, position window),
@@ -380,8 +390,8 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
 constexpr int kSubWinBits = 14, kSubWin = 1 << kSubWinBits, kMaxSubWins = 4;
 
 __host__ __device__ inline int parse_hl_words(int n) { return (n + 1 + 31) / 32; }
-// per-chunk event counts and regions, the chunk table (read, cs offset), the chunk counter
-__host__ __device__ constexpr int parse_misc_bytes() { return kMaxCh * 4 + kMaxCh * 8 + (kMaxCh + 2) * 8 + (kMaxCh + 4) * 4 + 16; }
+// the chunk table (cs offset, read), the chunk counter and the page counter
+__host__ __device__ constexpr int parse_misc_bytes() { return (kMaxCh + 2) * 8 + (kMaxCh + 4) * 4 + 16; }
 static_assert(parse_misc_bytes() % 16 == 0 && kMaxCh % 4 == 0, "parse LDS misc area alignment");
 template <int WIN>
 // position tallies of K_parse: 0 = global atomics, 4 = global atomics AND the
@@ -616,24 +626,71 @@ __device__ __forceinline__ void chunk_store(uint8_t* p, U8x32 v) {
   reinterpret_cast<uint4*>(p)[1] = v.b;
 }
 
-// events per thread per staged scatter chunk of the epilogue's bucket sort:
-// 12 -> one chunk per workgroup at C2 (parse phase 8 -> 12: C2 143.5 -> 141.9
-// us, C4 -0.7 %, C5 -0.9 %, C3 -0.3 %, C1 +0.8 %; 16 the same;
-// profiles/r04_experiments/kparse_epilogue_chunk.txt)
-#ifndef MPC_EPI_U
-#define MPC_EPI_U 12
-#endif
-// End of a parse workgroup: flush the LDS position
-// tallies and the LEFT-gap bitmap with contiguous atomics, then bucket-sort the
-// workgroup's insertion events by gap (counting sort, kBW gaps per bucket) from
-// its event regions (nreg regions: count wcnt[k] at ins_raw[wbase[k]]) into
-// ins_sorted, staging chunks of stg_cap events in LDS at stg.  Every thread of
-// the block calls it.
+// One insertion event into its (workgroup, bucket) page (every lane with an
+// event calls it; wave-uniform loop).  The bucket word W = page << 12 | fill:
+// a returning add takes slot `fill`; the lane that takes slot 64 of a full page
+// opens the next one (page counter npg, owner pg_own) and publishes it with
+// fill 1 (its own event in slot 0); lanes that found the page full meanwhile
+// (slot > 64, their adds are discarded by the publish) wait for the new page
+// and try again.  W lives in LDS (tally modes 0-3) or HBM (mode 4).  Every
+// wave reaches the loop's end: an opener never waits.
+template <bool GLOBAL_W>
+__device__ __forceinline__ void parse_place_event(const ParseArgs& a, bool has, uint32_t* W, uint32_t* npg,
+                                                  int64_t pbase, uint32_t pcap, int b, uint32_t word) {
+  // A waiting lane only looks at W once per pass of the wave-uniform loop, so
+  // an opener lane of the SAME wave (whose branch the compiler may place after
+  // the waiting lanes' code in one pass) publishes before the next look
+  bool need = has, waiting = false;
+  uint32_t wpg = 0;
+  int spins = 0;
+  while (ballot(need)) {
+    if (need && waiting) {
+      const uint32_t cur = GLOBAL_W ? __hip_atomic_load(W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                    : __hip_atomic_load(W, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      waiting = (cur >> kPgBits) == wpg;
+      if (waiting && ++spins > (1 << 22)) {  // bounded: never expected
+        atomicOr(&a.status[MPC_ST_FLAGS], DE_INTERNAL);
+        need = false;
+      }
+    }
+    if (need && !waiting) {
+      const uint32_t old = atomicAdd(W, 1u);
+      const uint32_t slot = old & ((1u << kPgBits) - 1u), pg = old >> kPgBits;
+      if (slot < (uint32_t)kPgEv) {
+        a.ins_sorted[(pbase + pg) * kPgEv + slot] = word;
+        need = false;
+      } else if (slot == (uint32_t)kPgEv) {
+        uint32_t np = atomicAdd(npg, 1u);
+        if (np >= pcap) {  // never expected: the page region bound (parse_page_base)
+          atomicOr(&a.status[MPC_ST_FLAGS], DE_INTERNAL);
+          np = pcap - 1;
+        }
+        a.pg_own[pbase + np] = (uint32_t)b;
+        a.ins_sorted[(pbase + np) * kPgEv] = word;
+        atomicExch(W, (np << kPgBits) | 1u);
+        need = false;
+      } else {
+        waiting = true;  // the page filled meanwhile: wait for its opener
+        wpg = pg;
+      }
+    }
+  }
+}
+
+// End of a parse workgroup: flush the LDS position tallies and the LEFT-gap
+// bitmap with contiguous atomics (tally modes 1-3), then list every bucket's
+// pages: bk_cnt = its events, bk_off = where its page list starts in
+// pg_list[pbase ...] -- the pages (global page numbers) in any order but the bucket's current
+// (possibly partial) page LAST, so event e of the bucket is in page
+// pg_list[pbase + bk_off + e / 64] at slot e % 64.  W (page words), cnt and cur
+// are LDS for modes 0-3 (cnt, cur alias the flushed tallies) and HBM for mode 4
+// (W = bk_cur, cnt = bk_cnt zeroed by K_clear, cur = bk_cur once read).  Every
+// thread of the block calls it.
 template <int TM>
-__device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, int64_t r0, uint32_t* hl,
-                               const uint32_t* bcnt, uint32_t* uni, const uint32_t* wcnt, const int64_t* wbase,
-                               int nreg, uint64_t* stg, int stg_cap) {
-  constexpr bool fused = TM != 0;
+__device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, uint32_t* hl, uint32_t* W, uint32_t* uni,
+                               const uint32_t* npg, int64_t pbase) {
+  constexpr bool big = TM == 4;
+  constexpr bool fused = TM >= 1 && TM <= 3;
   constexpr bool lds_sub = TM == 1 || TM == 2;
   constexpr bool packed = TM == 2 || TM == 3;
   const int l = lane();
@@ -658,138 +715,65 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, int64
       if (v) atomicAdd(sg + k, v);
     }
   }
-  for (int k = threadIdx.x; k < parse_hl_words(n); k += blockDim.x) {
+  for (int k = threadIdx.x; !big && k < parse_hl_words(n); k += blockDim.x) {
     const uint32_t v = hl[k];
     if (!v) continue;
     const int g0 = gb + 32 * k;  // global bit of local bit 0 of this word
     atomicOr(a.hasleft + (g0 >> 5), v << (g0 & 31));
     if (g0 & 31) atomicOr(a.hasleft + (g0 >> 5) + 1, v >> (32 - (g0 & 31)));
   }
+  const int64_t wgb = (int64_t)blockIdx.x * a.nbs;
+  uint32_t* cnt = big ? reinterpret_cast<uint32_t*>(a.bk_cnt) + wgb : uni;       // non-last pages per bucket
+  uint32_t* cur = big ? a.bk_cur + wgb : uni + nbk;                               // list cursors
+  auto wload = [&](int b) -> uint32_t {
+    return big ? __hip_atomic_load(W + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : W[b];
+  };
+  __syncthreads();  // (LDS tallies flushed: cnt / cur may alias them)
+  const uint32_t np_all = *npg;
+  // A: mark every bucket's last page (it goes to the end of the bucket's list)
+  for (int b = threadIdx.x; b < nbk; b += blockDim.x) {
+    const uint32_t w = wload(b);
+    if ((w >> kPgBits) != kPgNone) a.pg_own[pbase + (w >> kPgBits)] = kPgMark;
+    if (!big) cnt[b] = 0;
+  }
   __syncthreads();
-  // ---- bucket-sort this workgroup's insertion events by gap (counting sort) ----
-  // bucket counts: bcnt (main loop); cursors and the scatter's chunk tables alias the flushed tallies
-  uint32_t* bcur = uni;
-  const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;
-  const int bstride = (int)blockDim.x;
-  constexpr int kEpiU = MPC_EPI_U;  // events per thread per staged scatter chunk
-  if (threadIdx.x < 64) {  // exclusive scan over buckets by one wave
-    int carry_b = 0;
+  // B: the other pages per bucket
+  for (uint32_t p = threadIdx.x; p < np_all; p += blockDim.x) {
+    const uint32_t b = a.pg_own[pbase + p];
+    if (b != kPgMark) atomicAdd(cnt + b, 1u);
+  }
+  __syncthreads();
+  // C: one wave -- list offsets (exclusive scan of the page counts), event
+  // counts, the last page at the end of each list, the list cursors
+  if (threadIdx.x < 64) {
+    int carry = 0;
     for (int c0 = 0; c0 < nbk; c0 += 64) {
-      const int k = c0 + l;
-      const int v = k < nbk ? (int)bcnt[k] : 0;
-      const int inc = wave_scan_i32(v);
-      if (k < nbk) {
-        bcur[k] = (uint32_t)(carry_b + inc - v);
-        a.bk_cnt[(int64_t)blockIdx.x * a.nbs + k] = v;
-        a.bk_off[(int64_t)blockIdx.x * a.nbs + k] = carry_b + inc - v;
+      const int b = c0 + l;
+      uint32_t w = kPgInit, c = 0;
+      if (b < nbk) {
+        w = wload(b);
+        c = big ? (uint32_t)__hip_atomic_load(cnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : cnt[b];
       }
-      carry_b += wave_last_i32(inc);
+      const bool has = (w >> kPgBits) != kPgNone;
+      const int np = (int)c + (has ? 1 : 0);
+      const int inc = wave_scan_i32(np);
+      const int off = carry + inc - np;
+      if (b < nbk) {
+        a.bk_cnt[wgb + b] = has ? (int32_t)(c * kPgEv + (w & ((1u << kPgBits) - 1u))) : 0;
+        a.bk_off[wgb + b] = off;
+        if (has) a.pg_list[pbase + off + np - 1] = (uint32_t)(pbase + (w >> kPgBits));
+        if (big) __hip_atomic_store(cur + b, (uint32_t)off, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        else cur[b] = (uint32_t)off;
+      }
+      carry += wave_last_i32(inc);
     }
   }
-  if (threadIdx.x == 0) a.rbase[blockIdx.x] = rb_wg;
+  if (threadIdx.x == 0) a.rbase[blockIdx.x] = pbase;
   __syncthreads();
-  // scatter, staged: chunks of the workgroup's events (the wave regions
-  // concatenated) are counting-sorted by bucket in LDS (the per-wave areas are
-  // free now), then written out so that consecutive lanes store consecutive
-  // addresses of a bucket's run (8-byte scattered stores left most 128-byte
-  // lines partially written: ~8x HBM write amplification at C4)
-  uint32_t* dst = a.ins_sorted + rb_wg;
-  const int64_t rg0 = a.read_offset + r0;  // the workgroup's first (global) read
-  uint32_t* ccnt = bcur + nbk;  // [nbk] per-chunk bucket counts
-  uint32_t* coff = ccnt + nbk;  // [nbk + 1] their exclusive scan (coff[nbk]: events staged)
-  const int chunk = min(stg_cap, kEpiU * bstride);
-  for (int k = threadIdx.x; k < nbk; k += bstride) ccnt[k] = 0;
-  int Ev = 0;
-  for (int ww = 0; ww < nreg; ++ww) Ev += (int)wcnt[ww];
-  int ww_t = 0, pre_t = 0;  // this thread's walk over the regions (its k only grow)
-  __syncthreads();
-  for (int c0 = 0; c0 < Ev; c0 += chunk) {
-    const int c1 = min(c0 + chunk, Ev);
-    uint64_t ev[kEpiU];
-    uint32_t rk[kEpiU];
-#pragma unroll
-    for (int u = 0; u < kEpiU; ++u) {
-      const int k = c0 + (int)threadIdx.x + u * bstride;
-      ev[u] = ~0ull;
-      if (k < c1) {
-        while (k >= pre_t + (int)wcnt[ww_t]) { pre_t += (int)wcnt[ww_t]; ++ww_t; }
-        ev[u] = a.ins_raw[wbase[ww_t] + (k - pre_t)];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < kEpiU; ++u) {
-      const uint32_t gap = (uint32_t)(ev[u] >> 10) & kNullGap;
-      rk[u] = gap <= (uint32_t)n ? atomicAdd(ccnt + gap / kBW, 1u) : ~0u;
-    }
-    __syncthreads();
-    if (threadIdx.x < 64) {
-      int cb = 0;
-      for (int b0 = 0; b0 < nbk; b0 += 64) {
-        const int k = b0 + l;
-        const int v = k < nbk ? (int)ccnt[k] : 0;
-        const int inc = wave_scan_i32(v);
-        if (k < nbk) coff[k] = (uint32_t)(cb + inc - v);
-        cb += wave_last_i32(inc);
-      }
-      if (l == 0) coff[nbk] = (uint32_t)cb;
-    }
-    __syncthreads();
-#pragma unroll
-    for (int u = 0; u < kEpiU; ++u)
-      if (rk[u] != ~0u) stg[coff[((uint32_t)(ev[u] >> 10) & kNullGap) / kBW] + rk[u]] = ev[u];
-    __syncthreads();
-    const int staged = (int)coff[nbk];
-    for (int j = threadIdx.x; j < staged; j += bstride) {
-      const uint64_t e = stg[j];
-      const int b = (int)(((uint32_t)(e >> 10) & kNullGap) / kBW);
-      dst[bcur[b] + (j - (int)coff[b])] = sorted_event(e, rg0);
-    }
-    __syncthreads();
-    for (int k = threadIdx.x; k < nbk; k += bstride) { bcur[k] += ccnt[k]; ccnt[k] = 0; }
-    __syncthreads();
-  }
-}
-
-// Tally mode 4 (references beyond the LDS budget): the same bucket sort with
-// its counters in HBM.  The main loop counted every bucket's events into
-// bk_cur (zeroed by K_clear) with device atomics; one wave turns them into the
-// workgroup's bk_cnt / bk_off and scatter cursors, then every thread places its
-// raw events with a returning atomic on the cursor (K_left does not depend on
-// the order of a bucket's events, only on the slice they lie in).
-__device__ void parse_epilogue_big(const ParseArgs& a, int n, int nbk, int64_t r0, const uint32_t* wcnt,
-                                   const int64_t* wbase, int nreg) {
-  const int l = lane();
-  const int64_t wg = (int64_t)blockIdx.x * a.nbs;
-  const int64_t rb_wg = (a.cs_off[r0] - a.cs_base) / 2 + 3 * r0;
-  if (threadIdx.x < 64) {  // every wave's counting atomics completed before the barrier
-    int carry_b = 0;
-    for (int c0 = 0; c0 < nbk; c0 += 64) {
-      const int k = c0 + l;
-      const int v = k < nbk ? __hip_atomic_load(a.bk_cur + wg + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
-      const int inc = wave_scan_i32(v);
-      if (k < nbk) {
-        a.bk_cnt[wg + k] = v;
-        a.bk_off[wg + k] = carry_b + inc - v;
-        __hip_atomic_store(a.bk_cur + wg + k, carry_b + inc - v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      carry_b += wave_last_i32(inc);
-    }
-  }
-  if (threadIdx.x == 0) a.rbase[blockIdx.x] = rb_wg;
-  __syncthreads();
-  uint32_t* dst = a.ins_sorted + rb_wg;
-  const int64_t rg0 = a.read_offset + r0;
-  int Ev = 0;
-  for (int ww = 0; ww < nreg; ++ww) Ev += (int)wcnt[ww];
-  int ww_t = 0, pre_t = 0;
-  for (int k = threadIdx.x; k < Ev; k += blockDim.x) {
-    while (k >= pre_t + (int)wcnt[ww_t]) { pre_t += (int)wcnt[ww_t]; ++ww_t; }
-    const uint64_t ev = a.ins_raw[wbase[ww_t] + (k - pre_t)];
-    const uint32_t gap = (uint32_t)(ev >> 10) & kNullGap;
-    if (gap <= (uint32_t)n) {
-      const int pos = atomicAdd(a.bk_cur + wg + gap / kBW, 1);
-      dst[pos] = sorted_event(ev, rg0);
-    }
+  // D: place the other pages
+  for (uint32_t p = threadIdx.x; p < np_all; p += blockDim.x) {
+    const uint32_t b = a.pg_own[pbase + p];
+    if (b != kPgMark) a.pg_list[pbase + atomicAdd(cur + b, 1u)] = (uint32_t)(pbase + p);
   }
 }
 
@@ -818,9 +802,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int nw = (int)(blockDim.x >> 6);
   const int w = uniform_i32((int)(threadIdx.x >> 6));
   WL& W = *reinterpret_cast<WL*>(lds + w * (int)sizeof(WL));
-  uint32_t* wcnt = reinterpret_cast<uint32_t*>(lds + nw * (int)sizeof(WL));     // [kMaxCh] events per chunk
-  int64_t* wbase = reinterpret_cast<int64_t*>(wcnt + kMaxCh);                  // [kMaxCh] event region per chunk
-  int64_t* cbo = wbase + kMaxCh;                                                // [kMaxCh + 1] chunk bounds: cs offset
+  int64_t* cbo = reinterpret_cast<int64_t*>(lds + nw * (int)sizeof(WL));        // [kMaxCh + 1] chunk bounds: cs offset
   int32_t* cbr = reinterpret_cast<int32_t*>(cbo + kMaxCh + 2);                  // [kMaxCh + 1] ... and read
   uint32_t* cnext = reinterpret_cast<uint32_t*>(cbr + kMaxCh + 4);              // next chunk to take
   uint32_t* hl = cnext + 4;                                                      // LEFT gaps bitmap
@@ -834,9 +816,15 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int n = a.n_of[smp];
   const int gb = a.gbase[smp];
   const int nbk = (n + 1 + kBW - 1) / kBW;  // insertion buckets
-  uint32_t* bcnt = hl + parse_hl_words(n);  // [nbk] insertion events per bucket (counted as they are stored)
-  uint32_t* uni = bcnt + nbk;
-  constexpr bool big = TM == 4;             // per-gap state (LEFT bitmap, bucket counters) in HBM
+  constexpr bool big = TM == 4;             // per-gap state (LEFT bitmap, bucket page words) in HBM
+  // [nbk] page word of every insertion bucket (page << 12 | fill, parse_place_event)
+  uint32_t* bkw = big ? a.bk_cur + (int64_t)blockIdx.x * a.nbs : hl + parse_hl_words(n);
+  uint32_t* uni = hl + parse_hl_words(n) + nbk;
+  uint32_t* npg = cnext + 1;                // pages opened by the workgroup
+  // the workgroup's page region [pbase, pnext) (parse_page_base)
+  const int64_t pbase = parse_page_base(a.cs_off[r0] - a.cs_base, r0, blockIdx.x, a.nbs);
+  const int64_t pnext = parse_page_base(a.cs_off[r1] - a.cs_base, r1, blockIdx.x + 1, a.nbs);
+  const uint32_t pcap = (uint32_t)min(pnext - pbase, (int64_t)kPgNone);
   constexpr bool fused = TM >= 1 && TM <= 3;  // depth differences in LDS (one address space per instantiation)
   constexpr bool lds_sub = TM == 1 || TM == 2;  // substitution tallies in LDS too
   constexpr bool packed = TM == 2 || TM == 3;
@@ -847,8 +835,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   //          biased by 0x8000: at most 16383 reads per workgroup and 2 per read and
   //          position keep every partial sum inside (0, 0xffff): no carry across halves
   uint32_t* del_l = uni + nsub;
-  for (int k = threadIdx.x; !big && k < parse_hl_words(n) + nbk; k += blockDim.x) hl[k] = 0;  // hl, bcnt
-  if (threadIdx.x == 0) *cnext = (uint32_t)nw;  // chunks 0..nw-1 go to waves 0..nw-1
+  for (int k = threadIdx.x; !big && k < parse_hl_words(n); k += blockDim.x) hl[k] = 0;
+  for (int k = threadIdx.x; !big && k < nbk; k += blockDim.x) bkw[k] = kPgInit;  // (mode 4: K_clear)
+  if (threadIdx.x == 0) { *cnext = (uint32_t)nw; *npg = 0u; cnext[2] = 0u; }  // chunks 0..nw-1 go to waves 0..nw-1
   const int nch = wk.w;
   for (int k = threadIdx.x; k <= nch; k += blockDim.x) {
     const int32_t r = a.wave_tab[(int64_t)blockIdx.x * (kMaxCh + 1) + k];
@@ -858,7 +847,17 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   if (fused)
     for (int k = threadIdx.x; k < nsub + (packed ? (n + 2) / 2 : n + 1); k += blockDim.x)
       uni[k] = (packed && k >= nsub) ? 0x80008000u : 0u;
+  // a read with a negative tstart in the workgroup: its chunks take the rounds
+  // that follow Python's negative index wrap (NEG below; the others compile
+  // none of it)
+  // (an OR through cnext[2], not __syncthreads_or: that one takes static LDS
+  // the planner's budget does not hold)
+  bool has_neg = false;
+  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) has_neg |= a.tstart[r] < 0;
   __syncthreads();
+  if (ballot(has_neg) && lane() == 0) atomicOr(cnext + 2, 1u);
+  __syncthreads();
+  const bool wg_neg = uniform_i32((int)cnext[2]) != 0;
 
   auto odd_sub = [&](int pos, int code) {
     if (lds_sub) atomicAdd(sub_l + 2 * pos + (code >> 1), 1u << (16 * (code & 1)));
@@ -879,10 +878,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     if (big) atomicOr(a.hasleft + ((gb + pos) >> 5), 1u << ((gb + pos) & 31));
     else atomicOr(hl + (pos >> 5), 1u << (pos & 31));
   };
-  auto bucket_add = [&](int pos) {  // one more insertion event in pos's bucket
-    if (big) atomicAdd(a.bk_cur + (int64_t)blockIdx.x * a.nbs + pos / kBW, 1);
-    else atomicAdd(bcnt + pos / kBW, 1u);
-  };
   // The workgroup's reads come in chunks (planner: contiguous, by cs bytes,
   // 5/8 of the bytes in the first nw chunks, smaller ones after); wave w
   // starts on chunk w and takes the next free one when it is done, so all
@@ -898,18 +893,16 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     const uint32_t v = atomicAdd(cnext, l == 0 ? 1u : 0u);
     return uniform_i32(__builtin_amdgcn_readlane((int)v, 0));
   };
+  auto chunks = [&](auto negc) {
+  constexpr bool NEG = decltype(negc)::value;
   for (int chk = w < nch ? w : nch; chk < nch; chk = take_chunk()) {
   const int64_t ra = uniform_i32(cbr[chk]), rb = uniform_i32(cbr[chk + 1]);
   const int64_t wend = readlane64(cbo[chk + 1], 0);
   int64_t P = readlane64(cbo[chk], 0);
-  const int64_t ev_base = (P - a.cs_base) / 2 + 3 * ra;  // this chunk's event region in ins_raw
   const int64_t sev_base = (P - a.cs_base) / 3 + 2 * ra;  // ... and its substitution-event regions (TM 3)
   uint32_t nsub_v = 0;                                    // lane k: substitution events of window k
-  uint32_t nev = 0;                                       // events written (wave-uniform)
   int64_t rs0 = ra;         // first read whose cs starts at or after P
   bool carry = false;       // slot 0 holds a read continuing into this window
-  bool neg = false;         // a read with a negative tstart reached this chunk: the rounds follow
-                            // Python's negative index wrap (wave-uniform, sticky for the chunk)
   int32_t c_base = 0;       // ... and its coordinate base (wave-uniform): i = base + window prefix of advances
   constexpr bool dma = parse_dma<WIN>();
   int sb = 0;               // stage buffer of the current window
@@ -1011,7 +1004,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     }
     const bool inwin = l < 63 && cur.o < C;  // read rs0+l starts in [P, C)
     const int nst = __popcll(ballot(inwin));
-    neg = neg || ballot(inwin && cur.ts < 0) != 0;
     // ---- per-read slots ----
     if (inwin) {
       const int q = l + 1;
@@ -1294,11 +1286,14 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       // write slots into a wrapped ODD position: unsupported (MPC_DE_UNSUPPORTED)
       bool wrap = false, unsup = false;
       int di = i, gi = i, li = olen_e;  // deletion start, LEFT gap and length
-      if (neg) {
+      if constexpr (NEG) {
         const bool mat = (kind == 1) | (kind == 2);
         bad_i = ((adv0 > 0) & (((iu + n + 1) | (n - i)) < 0)) | (mat & (((i + n + 1) | (n - adv - i)) < 0)) |
                 ((kind == 3) & (((i + n) | (n - i)) < 0));
-        unsup = (kind == 3) & (i < 0) & (i + n >= 0);
+        // '+' into a wrapped odd position; or an advance clamped at kAdvCap
+        // from a negative coordinate (its true end may still be <= n)
+        unsup = ((kind == 3) & (i < 0) & (i + n >= 0)) | ((adv0 >= kAdvCap) & (iu < 0)) |
+                ((adv >= kAdvCap) & (i < 0) & ((kind == 1) | (kind == 4)));
         wrap = (kind == 2) & (i < 0);
         di = i < 0 ? 0 : i;
         gi = wrap ? i + n + 1 : i;
@@ -1308,7 +1303,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const int rl = q_read;
       const bool ok = te == 0;
       if (ok & (kind == 2) & !wrap & (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
-      const bool del = ok & (kind == 4) & (di < n) & (i + olen_e > di);
+      const bool del = NEG ? ok & (kind == 4) & (di < n) & (i + olen_e > di) : ok & (kind == 4) & (i >= 0) & (i < n);
       if (del) {
         depth_dec(di);
         depth_inc(i + olen_e < n ? i + olen_e : n);
@@ -1329,27 +1324,24 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         }
       }
       const bool ins_inline = ((kind == 3 && olen_e <= kInsInline) || wrap) && ok;
-      const uint64_t bins = ballot(ins_inline);
-      if (ins_inline) {
-        a.ins_raw[ev_base + nev + lanes_below(bins)] = ins_event(gi, li, pay, a.read_offset + rl);
-        bucket_add(gi);
-      }
+      if (ballot(ins_inline))  // the event into its bucket's page (written once)
+        parse_place_event<big>(a, ins_inline, bkw + gi / kBW, npg, pbase, pcap, gi / kBW,
+                               ins_word(gi, li, pay, rl - (int)r0));
       if (last) {  // the read's last operation: i_end, downstream check, span
         const int ia = i + adv;
         const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
         const int dnf = q_iend & (1 << 30);
         if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
         // ... or, wrapped, past the front / into an odd position (unsupported)
-        if (neg && dnf && ia < 0) te |= ia + n >= 0 ? DE_UNSUP : DE_INDEX;
+        if (NEG && dnf && ia < 0) te |= ia + n >= 0 ? DE_UNSUP : DE_INDEX;
         W.s_iend[q] = ie | dnf;
-        const int ts = q_ts < 0 ? 0 : q_ts;  // matches below 0 write nothing
+        const int ts = NEG && q_ts < 0 ? 0 : q_ts;  // matches below 0 write nothing
         const int e2 = ie > n ? n : ie;
         if (ts < e2) { depth_inc(ts); depth_dec(e2); }
       }
       if (te) flag_read(a, te, rl);
       G += atot;
       qc += __popcll(brs);
-      nev += (uint32_t)__popcll(bins);
       MPC_SEG(4);
     }
     wave_sync_lds();
@@ -1382,18 +1374,18 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     flag_read(a, DE_OP, r);
     a.i_end[r] = ts < 0 ? 0 : (ts > n ? n + 1 : ts);
   }
-  if (l == 0) { wcnt[chk] = nev; wbase[chk] = ev_base; }
   if (TM == 3 && l < a.sub_wins) a.subev_cnt[((int64_t)blockIdx.x * kMaxCh + chk) * kMaxSubWins + l] = nsub_v;
   }  // chunks
+  };
+  if (wg_neg) chunks(std::true_type{});
+  else chunks(std::false_type{});
   MPC_SEG(5);
   // every LDS-DMA was waited for by the window after it (one is issued only
   // when another window follows); drain anyway before the LDS is reused
   if (parse_dma<WIN>()) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   MPC_SEG(6);
-  if constexpr (big) parse_epilogue_big(a, n, nbk, r0, wcnt, wbase, nch);
-  else parse_epilogue<TM>(a, n, gb, nbk, r0, hl, bcnt, uni, wcnt, wbase, nch, reinterpret_cast<uint64_t*>(lds),
-                          nw * (int)sizeof(WL) / 8);
+  parse_epilogue<TM>(a, n, gb, nbk, hl, bkw, uni, npg, pbase);
 #ifdef MPC_STAMPS
   MPC_SEG(7);
   const int64_t gw = (int64_t)blockIdx.x * kMaxPW + w;
@@ -2087,10 +2079,10 @@ constexpr int kUnit = kUB * kEPT;     // events per work unit (K_left<kUB>; K_le
 struct UnitArgs {
   const int4* bc;  // {sample, bucket, pw0, pw1}
   const int32_t* n_of; const int32_t* gbase;
-  const int32_t* bk_cnt; int4* units; uint32_t* status;  // units: 2 int4 per unit (see read_unit)
+  const int32_t* bk_cnt; int4* units; uint32_t* status;  // units: 2 int4 per unit (see load_unit)
   int64_t n_bc, units_cap;
   int32_t nbs;
-  int32_t unit;  // events per work unit (K_left's threads x kEPT)
+  int32_t unit;  // pages per work unit (K_left's threads x kEPT / 64: one page per wave and step)
 };
 
 // kUE consecutive table entries per wave (one wave per entry at a time), one
@@ -2113,8 +2105,8 @@ __device__ __forceinline__ void units_block(const UnitArgs& a, int64_t blk) {
     if (ent < a.n_bc) {  // wave-uniform
       const int4 bc = a.bc[ent];
       bcs[e] = bc;
-      for (int pw = bc.z + l; pw < bc.w; pw += 64) t += a.bk_cnt[(int64_t)pw * a.nbs + bc.y];
-      t = wave_sum(t);
+      for (int pw = bc.z + l; pw < bc.w; pw += 64) t += (a.bk_cnt[(int64_t)pw * a.nbs + bc.y] + kPgEv - 1) / kPgEv;
+      t = wave_sum(t);  // the entry's pages
     }
     ts[e] = t;
     nus[e] = (t + a.unit - 1) / a.unit;
@@ -2155,29 +2147,30 @@ __global__ __launch_bounds__(kRS) void K_rsplit_units(Dev d, UnitArgs ua, int32_
   else units_block(ua, (int64_t)blockIdx.x - nrb);
 }
 
+struct UnitView { int smp, bucket, p0, np, n, gb, g0, gl, nsl; };
 // A unit record (2 int4, written by units_block): {sample, bucket, pw0, pw1},
-// {e0, cnt, n, gbase}.  Per unit: the entry's <= 256 slices (counts, sources)
-// lane-parallel, block scan (s_pre[256]: the entry's total); afterwards event e of the entry is
-// ins_sorted[s_src[j] + e - s_pre[j]] with j = the last slice whose s_pre <= e.
-// The per-gap tables of the bucket (global run range, this shard's sorted-RIGHT
-// range; K_ins: the anchor row) are loaded in the same round trip.
-struct UnitView { int smp, bucket, e0, cnt, n, gb, g0, gl, nsl; int64_t R0, R1; };
-template <bool ANC>
+// {p0, np, n, gbase}: pages [p0, p0 + np) of the entry's page sequence (its
+// slices -- parse workgroups pw0.. -- in order, each slice's pages as its list
+// in pg_list holds them: global page numbers, all full but the last).  One
+// round trip loads, per slice, its events, its list base and its workgroup's
+// first read, and the bucket's per-gap tables (global run range, this shard's
+// sorted-RIGHT range); a block scan gives the slices' first pages (s_ppre).
+// Wave w then takes the unit's pages w, w + NW, ... (unit_page: the slice of a
+// wave-uniform page by a search of s_ppre, its global page from pg_list), one
+// event per lane.
 __device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, const int32_t* bk_cnt,
                                               const int32_t* bk_off, const int64_t* rbase, int nbs,
                                               const int32_t* right_start, const int32_t* rsl, const int32_t* roff,
-                                              const int32_t* row_base, const int32_t* lo_f, const int32_t* rowcnt,
-                                              const int4* pwork, int32_t* s_r0,
-                                              int32_t* s_pre, int64_t* s_src, int32_t* s_wsum,
-                                              int32_t* s_rs, int32_t* s_rsl, int32_t* s_roff, int32_t* s_anc) {
+                                              const int4* pwork, int32_t* s_ppre, int32_t* s_cnt, int64_t* s_src,
+                                              int32_t* s_r0, int32_t* s_wsum, int32_t* s_rs, int32_t* s_rsl,
+                                              int32_t* s_roff) {
   const int4 ua = units[2 * u], ub = units[2 * u + 1];
   UnitView v;
-  v.smp = ua.x; v.bucket = ua.y; v.e0 = ub.x; v.cnt = ub.y; v.n = ub.z; v.gb = ub.w; v.nsl = ua.w - ua.z;
+  v.smp = ua.x; v.bucket = ua.y; v.p0 = ub.x; v.np = ub.y; v.n = ub.z; v.gb = ub.w; v.nsl = ua.w - ua.z;
   v.g0 = v.bucket * kBW;
   v.gl = v.g0 + kBW - 1 < v.n ? v.g0 + kBW - 1 : v.n;  // last gap of the bucket
   const int l = lane(), w = threadIdx.x >> 6;
   const int tid = (int)threadIdx.x;
-  // all global loads of the unit's tables first (one round trip)
   int cnt = 0, r0 = 0;
   int64_t src = 0;
   if (tid < 256) {  // <= 256 slices (parse workgroups) per table entry
@@ -2185,27 +2178,18 @@ __device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, cons
     if (pw < ua.w) {
       const int64_t slot = (int64_t)pw * nbs + v.bucket;
       cnt = bk_cnt[slot];
-      src = rbase[pw] + bk_off[slot];
+      src = rbase[pw] + bk_off[slot];  // the slice's page list in pg_list
       r0 = pwork[pw].y;
     }
   }
   const int64_t gg = (int64_t)v.gb + v.g0 + tid;
-  const bool gap_t = tid <= v.gl + 1 - v.g0;  // the bucket's gaps and the one after (range ends)
-  const bool anc_t = tid <= v.gl - v.g0;
-  v.R0 = v.R1 = 0;
-  if (ANC) {  // the bucket's row range (K_ins)
-    v.R0 = row_base[(int64_t)v.gb + v.g0];
-    v.R1 = (int64_t)row_base[(int64_t)v.gb + v.gl] + rowcnt[(int64_t)v.gb + v.gl];
-  }
-  int32_t x_rs = 0, x_rsl = 0, x_roff = 0, x_anc = 0;
-  if (gap_t) { x_rs = right_start[gg]; x_rsl = rsl[gg]; x_roff = roff[gg]; }
-  if (ANC && anc_t) x_anc = row_base[gg] + lo_f[gg] - 1;  // + hi of the run
-  if (gap_t) { s_rs[tid] = x_rs; s_rsl[tid] = x_rsl; s_roff[tid] = x_roff; }
-  if (ANC && anc_t) s_anc[tid] = x_anc;
+  if (tid <= v.gl + 1 - v.g0) { s_rs[tid] = right_start[gg]; s_rsl[tid] = rsl[gg]; s_roff[tid] = roff[gg]; }
+  const int npg = (cnt + kPgEv - 1) / kPgEv;
   if (tid < 256) {
-    const int inc = wave_scan_i32(cnt);
+    const int inc = wave_scan_i32(npg);
     if (l == 63) s_wsum[w] = inc;
-    s_pre[tid] = inc - cnt;
+    s_ppre[tid] = inc - npg;
+    s_cnt[tid] = cnt;
     s_src[tid] = src;
     s_r0[tid] = r0;
   }
@@ -2213,31 +2197,25 @@ __device__ __forceinline__ UnitView load_unit(const int4* units, int64_t u, cons
   if (tid < 256) {
     int wpre = 0;
     for (int k = 0; k < w; ++k) wpre += s_wsum[k];
-    s_pre[tid] += wpre;
-    if (tid == 255) s_pre[256] = s_pre[tid] + cnt;  // the entry's events
+    s_ppre[tid] += wpre;
   }
   __syncthreads();
   return v;
 }
-// the last slice j >= j0 with s_pre[j] <= e (j0 < 0: no hint): up to 3 linear
-// steps from the hint, else a binary search of the rest
-__device__ __forceinline__ int unit_slice_next(const int32_t* s_pre, int e, int j0) {
-  int lo = j0 < 0 ? 0 : j0;
-  if (j0 >= 0) {
+// page P of the unit's entry: its global page, events and slice's first read
+struct UnitPage { uint32_t page; int cnt, r0; };
+__device__ __forceinline__ UnitPage unit_page(const uint32_t* pg_list, const int32_t* s_ppre, const int32_t* s_cnt,
+                                              const int64_t* s_src, const int32_t* s_r0, int P) {
+  int j = 0;
 #pragma unroll
-    for (int t = 0; t < 3; ++t) {
-      if (lo == 255 || s_pre[lo + 1] > e) return lo;
-      ++lo;
-    }
-  }
-  int hi = 255;
-  while (lo < hi) {
-    const int mid = (lo + hi + 1) >> 1;
-    if (s_pre[mid] <= e) lo = mid; else hi = mid - 1;
-  }
-  return lo;
+  for (int h = 128; h >= 1; h >>= 1) j = s_ppre[j + h] <= P ? j + h : j;
+  const int k = P - s_ppre[j];
+  UnitPage r;
+  r.page = pg_list[s_src[j] + k];
+  r.cnt = min(kPgEv, s_cnt[j] - kPgEv * k);
+  r.r0 = s_r0[j];
+  return r;
 }
-
 
 // ---------------------------------------------------------------------------
 // K_left: LEFT events -> per-run max length M (the slot layout's input; the
@@ -2252,7 +2230,8 @@ struct LeftArgs {
   const int64_t* up_off; const int32_t* sample; const int32_t* tstart;
   const int32_t* n_of; const int32_t* gbase;
   const int4* bc; const int4* units; const uint32_t* status;
-  const uint32_t* ins_sorted; const int32_t* bk_cnt; const int32_t* bk_off; const int64_t* rbase;
+  const uint32_t* ins_sorted; const uint32_t* pg_list; const int32_t* bk_cnt; const int32_t* bk_off;
+  const int64_t* rbase;
   const int4* pwork;  // parse work table {sample, r0, r1, 0}: a slice's first read
   int64_t N, read_offset, ovf_cap;
   int32_t nbs;
@@ -2273,11 +2252,15 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
   // different bank (unpadded, all gaps' run-0 counters shared 16 banks)
   constexpr int kMs = kKMax + 1, kTs = kKMax * 16 + 1;
   __shared__ uint32_t Ml[kBW * kMs];
-  __shared__ int32_t s_pre[257];
-  __shared__ int64_t s_src[256];
-  __shared__ int32_t s_r0[256];  // per slice: its parse workgroup's first read
-  __shared__ int32_t s_wsum[4];
   __shared__ int32_t s_rs[kBW + 1], s_rsl[kBW + 1], s_roff[kBW + 1];  // per gap of the bucket (K_left)
+  __shared__ int32_t s_ppre[257], s_cnt[256], s_r0[256], s_wsum[4];   // per slice: first page, events, first read
+  __shared__ int64_t s_src[256];                                      // ... and its page list in pg_list
+  // 1024-thread blocks (C1-C4: few, large units) stage the unit's pages once,
+  // all threads in parallel (one barrier); 512-thread blocks (C5: many small
+  // units) look each page up in the wave that takes it (no barrier)
+  constexpr bool kStage = UB == 1024;
+  constexpr int kUP = kStage ? UB * kEPT / kPgEv : 1;
+  __shared__ uint4 s_pe[kUP];             // staged: {global page, events, first read, 0}
   __shared__ uint32_t Tl[kBW * kTs];  // per (gap, run): inline bases [bi from the 3' end][code]
   // 512-thread blocks: a smaller stage, so three blocks fit a CU's LDS
   constexpr int kLV = UB == 512 ? 3072 : kLeftVals;
@@ -2307,53 +2290,41 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       for (int k = threadIdx.x; k < kBW * kTs; k += blockDim.x) Tl[k] = 0;
     }
     MPC_LSEG(0);
-    const UnitView uv = load_unit<false>(a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, a.right_start, a.rsl,
-                                         a.roff, nullptr, nullptr, nullptr, a.pwork, s_r0, s_pre, s_src, s_wsum, s_rs,
-                                         s_rsl, s_roff, nullptr);
+    const UnitView uv = load_unit(a.units, u, a.bk_cnt, a.bk_off, a.rbase, a.nbs, a.right_start, a.rsl, a.roff,
+                                  a.pwork, s_ppre, s_cnt, s_src, s_r0, s_wsum, s_rs, s_rsl, s_roff);
     MPC_LSEG(1);
     const int n = uv.n;
     const int gb = uv.gb;
     const int g0 = uv.g0;
     uint32_t evs[kEPT];
-    int32_t jsq[kEPT];  // slice of each event (its workgroup's first read)
-    // all loads first (latency), then the tallies.  The thread's events move
-    // UB apart: with >= UB events per slice on average (C3 / C4) its slice is
-    // searched once, then advanced; with short slices (C2) every event's search
-    // is independent (a chain of advancing searches would serialize them)
-    const bool adv = s_pre[256] >= UB * uv.nsl;
-    if (kLean && !adv) {
-      // short slices: every event's slice by a branch-free 8-step binary
-      // search over the 256 slices (the last j with s_pre[j] <= e), the kEPT
-      // searches interleaved -- 8 dependent LDS round trips per unit
-#pragma unroll
-      for (int q = 0; q < kEPT; ++q) jsq[q] = 0;
-#pragma unroll
-      for (int h = 128; h >= 1; h >>= 1) {
-#pragma unroll
-        for (int q = 0; q < kEPT; ++q) {
-          const int e = uv.e0 + (int)threadIdx.x + q * UB;
-          const int m = jsq[q] + h;
-          jsq[q] = s_pre[m] <= e ? m : jsq[q];
-        }
+    int32_t r0q[kEPT];  // the first read of each event's parse workgroup
+    // all loads first (latency), then the tallies: wave w takes the unit's
+    // pages w, w + NW, ... (wave-uniform: their slice searches and page numbers
+    // are uniform), lane l the page's event l
+    constexpr int NW = UB / 64;
+    const int wv = uniform_i32((int)(threadIdx.x >> 6)), ln = lane();
+    if constexpr (kStage) {
+      for (int t = threadIdx.x; t < min(uv.np, kUP); t += UB) {
+        const UnitPage pg = unit_page(a.pg_list, s_ppre, s_cnt, s_src, s_r0, uv.p0 + t);
+        s_pe[t] = make_uint4(pg.page, (uint32_t)pg.cnt, (uint32_t)pg.r0, 0u);
       }
+      __syncthreads();
+    }
 #pragma unroll
-      for (int q = 0; q < kEPT; ++q) {
-        const int e = uv.e0 + (int)threadIdx.x + q * UB;
-        evs[q] = ~0u;
-        if (e < uv.e0 + uv.cnt) evs[q] = a.ins_sorted[s_src[jsq[q]] + (e - s_pre[jsq[q]])];
-      }
-    } else {
-      int js = -1;
-#pragma unroll
-      for (int q = 0; q < kEPT; ++q) {
-        const int e = uv.e0 + (int)threadIdx.x + q * UB;
-        evs[q] = ~0u;
-        jsq[q] = 0;
-        if (e < uv.e0 + uv.cnt) {
-          js = unit_slice_next(s_pre, e, adv ? js : -1);
-          jsq[q] = js;
-          evs[q] = a.ins_sorted[s_src[js] + (e - s_pre[js])];
+    for (int q = 0; q < kEPT; ++q) {
+      const int t = wv + NW * q;
+      evs[q] = ~0u;
+      r0q[q] = 0;
+      if (t < uv.np) {
+        UnitPage pg;
+        if constexpr (kStage) {
+          const uint4 e = s_pe[t];
+          pg.page = e.x; pg.cnt = (int)e.y; pg.r0 = (int)e.z;
+        } else {
+          pg = unit_page(a.pg_list, s_ppre, s_cnt, s_src, s_r0, uv.p0 + t);
         }
+        r0q[q] = pg.r0;
+        if (ln < pg.cnt) evs[q] = a.ins_sorted[(int64_t)pg.page * kPgEv + ln];
       }
     }
     // the run of an event at a mixed gap is a search of the gap's RIGHT reads:
@@ -2379,7 +2350,7 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       if (ev == ~0u) continue;
       const int gap = g0 + (int)((ev >> 10) & (kBW - 1));
       const int64_t g = (int64_t)gb + gap;
-      const int32_t rg = (int32_t)a.read_offset + s_r0[jsq[q]] + (int32_t)(ev >> 16);  // global reads < 2^30
+      const int32_t rg = (int32_t)a.read_offset + r0q[q] + (int32_t)(ev >> 16);  // global reads < 2^30
       const int L = (int)((ev >> 8) & 3u) + 1;
       const int p = gap - g0;
       const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
@@ -3167,7 +3138,7 @@ struct mpc_plan {
   mpc_input in;
   std::vector<int64_t> ref_len, read_begin;
   std::vector<int32_t> h_n, h_gbase;
-  int64_t N = 0, Ng = 0, G = 0, row_cap = 0, runs_cap = 0, ins_cap = 0, ovf_cap = 0;
+  int64_t N = 0, Ng = 0, G = 0, row_cap = 0, runs_cap = 0, ins_cap = 0, ovf_cap = 0, pages_cap = 0;
   int32_t S = 0;
   int32_t overrides = 0;  // MPC_OVR_* (experiment builds only)
   uint32_t sentinel = 0;
@@ -3187,12 +3158,12 @@ struct mpc_plan {
   int32_t shard = 0, n_shards = 1;
   int tally_mode = 0;  // K_parse TM
   enum {
-    B_STATUS, B_NOF, B_GBASE, B_IEND, B_INSRAW, B_INSSORT, B_BKCNT, B_BKOFF, B_RBASE, B_OVF, B_OVFCNT,
+    B_STATUS, B_NOF, B_GBASE, B_IEND, B_PGOWN, B_INSSORT, B_BKCNT, B_BKOFF, B_RBASE, B_OVF, B_OVFCNT,
     B_HASLEFT, B_KIN, B_VIN, B_KOUT, B_VOUT, B_KTMP, B_VTMP, B_BCNT, B_BPRE, B_RLEN, B_RPOS, B_RSTART, B_RSLOC, B_ROFF, B_RCNT, B_RCNTALL,
     // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
     B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
     B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_SROW, B_WPARSE, B_WBC, B_UNITS, B_RUNT,
-    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_SUBSLAB, B_WSUBSUM, B_GCNT, B_KSLOT, B_RSFLAG, B_COUNT
+    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_SUBSLAB, B_WSUBSUM, B_GCNT, B_KSLOT, B_RSFLAG, B_PGLIST, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -3247,9 +3218,10 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.cs_base = d.cs_base; a.ovf_cap = d.ovf_cap; a.read_offset = d.read_offset; a.n_reads = d.N;
   a.nbs = p->nbmax;
   a.i_end = d.i_end;
-  a.ins_raw = at<uint64_t>(p, mpc_plan::B_INSRAW); a.ins_sorted = at<uint32_t>(p, mpc_plan::B_INSSORT);
+  a.ins_sorted = at<uint32_t>(p, mpc_plan::B_INSSORT);
+  a.pg_own = at<uint32_t>(p, mpc_plan::B_PGOWN); a.pg_list = at<uint32_t>(p, mpc_plan::B_PGLIST);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
-  a.rbase = at<int64_t>(p, mpc_plan::B_RBASE); a.bk_cur = at<int32_t>(p, mpc_plan::B_BKCUR);
+  a.rbase = at<int64_t>(p, mpc_plan::B_RBASE); a.bk_cur = at<uint32_t>(p, mpc_plan::B_BKCUR);
   a.ovf = d.ovf; a.ovf_cnt = d.ovf_cnt; a.hasleft = d.hasleft; a.status = d.status;
   a.diff = d.diff; a.sub = d.sub;
   a.subev = at<uint16_t>(p, mpc_plan::B_SUBEV); a.subev_cnt = at<uint32_t>(p, mpc_plan::B_SUBCNT);
@@ -3307,7 +3279,7 @@ static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
   LeftArgs a;
   a.up_off = d.up_off; a.sample = d.sample; a.tstart = d.tstart; a.n_of = d.n_of; a.gbase = d.gbase;
   a.bc = at<const int4>(p, mpc_plan::B_WBC); a.units = at<const int4>(p, mpc_plan::B_UNITS); a.status = d.status;
-  a.ins_sorted = at<uint32_t>(p, mpc_plan::B_INSSORT);
+  a.ins_sorted = at<uint32_t>(p, mpc_plan::B_INSSORT); a.pg_list = at<uint32_t>(p, mpc_plan::B_PGLIST);
   a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT); a.bk_off = at<int32_t>(p, mpc_plan::B_BKOFF);
   a.rbase = at<int64_t>(p, mpc_plan::B_RBASE); a.pwork = at<const int4>(p, mpc_plan::B_WPARSE);
   a.N = d.N; a.read_offset = d.read_offset; a.ovf_cap = d.ovf_cap; a.nbs = p->nbmax;
@@ -3321,7 +3293,8 @@ static UnitArgs unit_args(const mpc_plan* p, const Dev& d) {
   a.bc = at<const int4>(p, mpc_plan::B_WBC); a.bk_cnt = at<int32_t>(p, mpc_plan::B_BKCNT);
   a.units = at<int4>(p, mpc_plan::B_UNITS); a.status = d.status;
   a.n_of = d.n_of; a.gbase = d.gbase;
-  a.n_bc = p->n_bc; a.units_cap = p->units_cap; a.nbs = p->nbmax; a.unit = p->left_ub * kEPT;
+  a.n_bc = p->n_bc; a.units_cap = p->units_cap; a.nbs = p->nbmax; a.unit = p->left_ub * kEPT / kPgEv;
+
   return a;
 }
 // K_left's geometry (planner: left_ub)
@@ -3652,7 +3625,9 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
       for (int s = 0; s < p->S; ++s) nb_all += (p->ref_len[s] + 1 + kBW - 1) / kBW;
       p->left_ub = nb_all > 4 * 512 && in->cs_bytes / nb_all < (256 << 10) ? 512 : kUB;
     }
-    p->units_cap = p->ins_cap / (p->left_ub * kEPT) + p->n_bc + 1;
+    // work units of left_ub * kEPT / 64 pages (parse_page_base bounds the pages)
+    p->units_cap = (parse_page_base(in->cs_bytes, p->N, p->n_parse_wg, p->nbmax) + 1) / (p->left_ub * kEPT / kPgEv) +
+                   p->n_bc + 1;
   }
   const int64_t N = p->N, Ng = p->Ng, G = p->G, R = p->row_cap, RU = p->runs_cap;
   const int64_t nbg = (G + kGB - 1) / kGB, nbk = (R + kKB - 1) / kKB;
@@ -3661,8 +3636,12 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_NOF, p->S, 4);
   set(mpc_plan::B_GBASE, p->S + 1, 4);
   set(mpc_plan::B_IEND, N, 4);
-  set(mpc_plan::B_INSRAW, p->ins_cap, 8);
-  set(mpc_plan::B_INSSORT, p->ins_cap, 4);
+  // insertion events in 64-event pages per (parse workgroup, bucket)
+  // (parse_page_base: the last workgroup's region ends at this bound)
+  p->pages_cap = parse_page_base(in->cs_bytes, N, p->n_parse_wg, p->nbmax) + 1;
+  set(mpc_plan::B_PGOWN, p->pages_cap, 4);
+  set(mpc_plan::B_PGLIST, p->pages_cap, 4);
+  set(mpc_plan::B_INSSORT, p->pages_cap * kPgEv, 4);
   set(mpc_plan::B_BKCNT, (int64_t)p->n_parse_wg * p->nbmax, 4);
   set(mpc_plan::B_BKOFF, (int64_t)p->n_parse_wg * p->nbmax, 4);
   set(mpc_plan::B_RBASE, p->n_parse_wg, 8);
@@ -3866,7 +3845,10 @@ int mpc_parse(mpc_plan* p, void* stream) {
     add(d.sub, 4 * p->G, 0u);
     add(d.maxR, p->G, 0u);
     if (p->rsort_multi) add(d.gcnt, p->G + 1, 0u);
-    if (p->tally_mode == 4) add(at<int32_t>(p, mpc_plan::B_BKCUR), (int64_t)p->n_parse_wg * p->nbmax, 0u);
+    if (p->tally_mode == 4) {  // the bucket page words and page counts of the HBM-state parse
+      add(at<int32_t>(p, mpc_plan::B_BKCUR), (int64_t)p->n_parse_wg * p->nbmax, kPgInit);
+      add(at<int32_t>(p, mpc_plan::B_BKCNT), (int64_t)p->n_parse_wg * p->nbmax, 0u);
+    }
     add(d.maxdepth, p->S, 0u);
     add(d.ksum, 2 * p->cnt[mpc_plan::B_KSUM], 0u);  // look-back status words (epoch-tagged as well)
     add(d.bsum, 2 * p->cnt[mpc_plan::B_BSUM], 0u);

@@ -339,7 +339,7 @@ def test_max_reference_dense_windows(pkg):
     for k in range(6):
         cs.append(b"Z::1000-" + b"a" * 1000 + b":%d" % (n - 2000)); ts.append(0)
         cs.append(b"Z::2097150*" + b"gat"[k % 3: k % 3 + 1] + b"g" + b":%d" % (n - 2097151)); ts.append(0)
-    cs.append(b"Z::%d" % (n + 5)); ts.append(-5)  # matches below 0 write nothing
+    cs.append(b"Z::%d" % (n + 1)); ts.append(-1)  # matches below 0 write nothing
     cs.append(b"Z::%d" % (n - 3)); ts.append(3)
     off = np.concatenate([[0], np.cumsum([len(c) for c in cs])]).astype(np.int64)
     z = np.zeros(len(cs) + 1, np.int64)
@@ -352,6 +352,13 @@ def test_max_reference_dense_windows(pkg):
     exp = _oracle(smp, -1.0, 1.0)
     assert exp["max_depth"] == 130 + 12 + 2
     _cmp(got, exp, "max_ref_dense")
+    # an advance past the 2^22 clamp from a negative coordinate: its true end
+    # (here exactly n) is not representable -> rejected, never a wrong count
+    bad = dict(smp, cs=np.frombuffer(b"Z::%d" % (n + 5), np.uint8).copy(), cs_off=np.array([0, 10], np.int64),
+               tstart=np.array([-5], np.int64), up_off=np.zeros(2, np.int64), down_off=np.zeros(2, np.int64))
+    with pytest.raises(pkg.engine.DataError) as e:
+        pkg.engine.pileup([bad], -1.0, 1.0)
+    assert e.value.flags & pkg.engine.DE_UNSUPPORTED
 
 
 def test_reference_past_coordinate_limit(pkg):

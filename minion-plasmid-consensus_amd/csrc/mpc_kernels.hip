@@ -327,10 +327,14 @@ template <int WIN> constexpr int tok_cap() { return WIN <= 1024 ? WIN : 1024; }
 #define MPC_PARSE_DMA 0
 #endif
 template <int WIN> constexpr bool parse_dma() { return MPC_PARSE_DMA && WIN >= 1024; }
-// K_parse tally modes (bit TM) whose rounds try the fast decode first
-// (measured: C4 -4.5 %, C5 -2 %, C3 +0.6 %, C2 (mode 1) +8 %)
+// K_parse tally modes (bit TM) whose rounds try the fast decode first.  Round
+// 4: modes 3-4 only (C4 -4.5 %, C5 -2 %, C3 +0.6 %, C2 (mode 1) +8 %: every
+// read starts with the empty tokens "Z" ":", which sent its round to the
+// general decode).  Round 5, with those tokens decoded as no-ops on the fast
+// path: every mode (C2 parse 137.9 -> 133.7 us, C1 -1 %, modes 3-4 +-0.2 %;
+// profiles/r05_experiments/place2_fdall_*.log)
 #ifndef MPC_FAST_DECODE_MODES
-#define MPC_FAST_DECODE_MODES 0x18
+#define MPC_FAST_DECODE_MODES 0x1f
 #endif
 template <int TM> constexpr bool fast_decode() { return (MPC_FAST_DECODE_MODES >> TM) & 1; }
 // ... and tally modes whose rounds find a unit's read base by an LDS round trip
@@ -636,11 +640,19 @@ __device__ __forceinline__ void chunk_store(uint8_t* p, U8x32 v) {
 // wave reaches the loop's end: an opener never waits.
 template <bool GLOBAL_W>
 __device__ __forceinline__ void parse_place_event(const ParseArgs& a, bool has, uint32_t* W, uint32_t* npg,
-                                                  int64_t pbase, uint32_t pcap, int b, uint32_t word) {
-  // A waiting lane only looks at W once per pass of the wave-uniform loop, so
-  // an opener lane of the SAME wave (whose branch the compiler may place after
-  // the waiting lanes' code in one pass) publishes before the next look
-  bool need = has, waiting = false;
+                                                  int64_t pbase, uint32_t* pg0, uint32_t pcap, int b, uint32_t word) {
+  // common case straight-line: the add gives a slot of the current page
+  // (pg0 = the workgroup's first page: 32-bit offsets from a scalar base)
+  uint32_t old = has ? atomicAdd(W, 1u) : 0u;
+  const bool fast = has && (old & ((1u << kPgBits) - 1u)) < (uint32_t)kPgEv;
+  if (fast) pg0[(old >> kPgBits) * kPgEv + (old & ((1u << kPgBits) - 1u))] = word;
+  bool need = has && !fast;
+  if (!ballot(need)) return;
+  // the page is full: open the next one, or wait for its opener.  A waiting
+  // lane looks at W once per pass of the wave-uniform loop, so an opener lane
+  // of the SAME wave (whose branch the compiler may place after the waiting
+  // lanes' code in one pass) has published before the next look
+  bool waiting = false, first = true;
   uint32_t wpg = 0;
   int spins = 0;
   while (ballot(need)) {
@@ -654,10 +666,11 @@ __device__ __forceinline__ void parse_place_event(const ParseArgs& a, bool has, 
       }
     }
     if (need && !waiting) {
-      const uint32_t old = atomicAdd(W, 1u);
+      if (!first) old = atomicAdd(W, 1u);
+      first = false;
       const uint32_t slot = old & ((1u << kPgBits) - 1u), pg = old >> kPgBits;
       if (slot < (uint32_t)kPgEv) {
-        a.ins_sorted[(pbase + pg) * kPgEv + slot] = word;
+        pg0[pg * kPgEv + slot] = word;
         need = false;
       } else if (slot == (uint32_t)kPgEv) {
         uint32_t np = atomicAdd(npg, 1u);
@@ -666,7 +679,7 @@ __device__ __forceinline__ void parse_place_event(const ParseArgs& a, bool has, 
           np = pcap - 1;
         }
         a.pg_own[pbase + np] = (uint32_t)b;
-        a.ins_sorted[(pbase + np) * kPgEv] = word;
+        pg0[np * kPgEv] = word;
         atomicExch(W, (np << kPgBits) | 1u);
         need = false;
       } else {
@@ -825,6 +838,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int64_t pbase = parse_page_base(a.cs_off[r0] - a.cs_base, r0, blockIdx.x, a.nbs);
   const int64_t pnext = parse_page_base(a.cs_off[r1] - a.cs_base, r1, blockIdx.x + 1, a.nbs);
   const uint32_t pcap = (uint32_t)min(pnext - pbase, (int64_t)kPgNone);
+  uint32_t* const pg0 = a.ins_sorted + pbase * kPgEv;  // the region's first event slot
   constexpr bool fused = TM >= 1 && TM <= 3;  // depth differences in LDS (one address space per instantiation)
   constexpr bool lds_sub = TM == 1 || TM == 2;  // substitution tallies in LDS too
   constexpr bool packed = TM == 2 || TM == 3;
@@ -1325,7 +1339,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       }
       const bool ins_inline = ((kind == 3 && olen_e <= kInsInline) || wrap) && ok;
       if (ballot(ins_inline))  // the event into its bucket's page (written once)
-        parse_place_event<big>(a, ins_inline, bkw + gi / kBW, npg, pbase, pcap, gi / kBW,
+        parse_place_event<big>(a, ins_inline, bkw + gi / kBW, npg, pbase, pg0, pcap, gi / kBW,
                                ins_word(gi, li, pay, rl - (int)r0));
       if (last) {  // the read's last operation: i_end, downstream check, span
         const int ia = i + adv;

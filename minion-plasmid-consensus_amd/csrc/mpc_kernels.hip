@@ -327,6 +327,7 @@ template <int WIN> constexpr int tok_cap() { return WIN <= 1024 ? WIN : 1024; }
 #define MPC_PARSE_DMA 0
 #endif
 template <int WIN> constexpr bool parse_dma() { return MPC_PARSE_DMA && WIN >= 1024; }
+
 // K_parse tally modes (bit TM) whose rounds try the fast decode first.  Round
 // 4: modes 3-4 only (C4 -4.5 %, C5 -2 %, C3 +0.6 %, C2 (mode 1) +8 %: every
 // read starts with the empty tokens "Z" ":", which sent its round to the
@@ -364,8 +365,7 @@ struct alignas(16) WaveLds {            // per-wave LDS of K_parse
   int32_t s_iend[kSlots];               // i_end | bit 30: read has a downstream flank
   int64_t s_end[kSlots];                // cs offset of the read's end
   uint8_t stage[stage_bufs<WIN>()][WIN + 16];  // window bytes (+16: word reads past the end)
-  uint8_t em[WIN / 8];                  // boundary bits (special characters | read starts), bit = byte
-  uint8_t ra[WIN / 8];                  // read-start bits
+  uint8_t ra[WIN / 8];                  // read-start bits, bit = byte
   uint16_t tok[tok_cap<WIN>() + 2 + 64];  // unit starts in [P, C), then the sentinel C; bits 12-14: ':' prefix
                                         // operand length, bit 15: read start (+64: unconditional loads)
 };
@@ -929,9 +929,11 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     const int64_t o63 = readlane64(cur.o, 63);
     if (o63 < E) E = o63;
     MPC_SEG(0);
-    const int64_t o_nx = __shfl(cur.o, (l + 1) & 63, 64);
-    const uint32_t uo_nx = (uint32_t)__shfl((int)cur.uo, (l + 1) & 63, 64);
-    const uint32_t dno_nx = (uint32_t)__shfl((int)cur.dno, (l + 1) & 63, 64);
+    // the next read's offsets (lane l + 1, by DPP; lane 63 is never a read of the window)
+    const int64_t o_nx = (int64_t)(((uint64_t)from_lane_above((uint32_t)((uint64_t)cur.o >> 32)) << 32) |
+                                   from_lane_above((uint32_t)cur.o));
+    const uint32_t uo_nx = from_lane_above(cur.uo);
+    const uint32_t dno_nx = from_lane_above(cur.dno);
     if (E <= P) {
       // reads rs0 .. rs0+62 all start at P: 63 empty cs (processOperation('', ''))
       if (l < 63) {
@@ -952,20 +954,16 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     uint32_t spm, cm_own;
     chunk_classes(cur.d, &spm, &cm_own);
     const uint32_t om_own = spm & ~cm_own;
-    put_lane_bits<CH>(W.em, l, spm);
     put_lane_bits<CH>(W.ra, l, 0u);
     wave_sync_lds();
     {  // read-start bits of every read starting inside the window (incl. E)
       const int64_t rel = cur.o - A;
-      if (rel >= 0 && rel < WIN) {
-        atomicOr(reinterpret_cast<uint32_t*>(W.em) + (rel >> 5), 1u << (rel & 31));
-        atomicOr(reinterpret_cast<uint32_t*>(W.ra) + (rel >> 5), 1u << (rel & 31));
-      }
+      if (rel >= 0 && rel < WIN) atomicOr(reinterpret_cast<uint32_t*>(W.ra) + (rel >> 5), 1u << (rel & 31));
     }
     wave_sync_lds();
     const int64_t cA = A + CH * l;
-    const uint32_t em_own = get_lane_bits<CH>(W.em, l);
     const uint32_t ra_own = get_lane_bits<CH>(W.ra, l);
+    const uint32_t em_own = spm | ra_own;  // boundaries: special characters and read starts
     // ---- cut C: E if E is a boundary (a read start), else the last boundary in (P, E) ----
     const bool e_rs = (E == wend) || (E == o63);
     int64_t C;
@@ -1084,14 +1082,17 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const int cnt = __popc(tu);
       const int incl = wave_scan_i32(cnt);
       T = wave_last_i32(incl);
-      int idx = incl - cnt;
       const int base = CH * l;
+      auto entry = [&](int k) -> uint16_t {
+        return (uint16_t)((uint32_t)(base + k) | (((pl0 >> k) & 1u) << 12) | (((pl1 >> k) & 1u) << 13) |
+                          (((p5 >> k) & 1u) << 14) | (((ra_own >> k) & 1u) << 15));
+      };
       uint32_t m = tu;
+      int idx = incl - cnt;
       while (m) {
         const int k = __ffs(m) - 1;
         m &= m - 1;
-        W.tok[idx++] = (uint16_t)((uint32_t)(base + k) | (((pl0 >> k) & 1u) << 12) | (((pl1 >> k) & 1u) << 13) |
-                                  (((p5 >> k) & 1u) << 14) | (((ra_own >> k) & 1u) << 15));
+        W.tok[idx++] = entry(k);
       }
       if (l == 0) W.tok[T] = far ? (uint16_t)(kFar | (c_rs ? 0x8000u : 0u)) : (uint16_t)((C - A) | (c_rs ? 0x8000u : 0u));
     }

@@ -2338,7 +2338,7 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
         } else {
           pg = unit_page(a.pg_list, s_ppre, s_cnt, s_src, s_r0, uv.p0 + t);
         }
-        r0q[q] = pg.r0;
+        r0q[q] = __builtin_amdgcn_readfirstlane(pg.r0);  // wave-uniform: SGPRs (K_left<1024> spilled 12 VGPRs)
         if (ln < pg.cnt) evs[q] = a.ins_sorted[(int64_t)pg.page * kPgEv + ln];
       }
     }

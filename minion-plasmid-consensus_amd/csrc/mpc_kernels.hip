@@ -50,8 +50,8 @@
 #define MPC_BF_TUNING_ 0
 #endif
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
-    defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) || defined(MPC_FLANK_BYTES4) ||     \
-    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES)
+    defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
+    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -2674,21 +2674,38 @@ __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Flank tallies, read-parallel.  Every read's upstream flank (LEFT at gap
-// tstart, :303 -> :37-62) and downstream flank (RIGHT at gap i_end, :323 ->
-// :64-72) map LINEARLY onto rows once the layout is known: byte j of the flank
-// goes to row rowstart + j, with
+// Flank tallies.  Every read's upstream flank (LEFT at gap tstart, :303 ->
+// :37-62) and downstream flank (RIGHT at gap i_end, :323 -> :64-72) map
+// LINEARLY onto rows once the layout is known: byte j of the flank goes to row
+// rowstart + j, with
 //   upstream   rowstart = row_base + lo_f + hi_run - L
 //   downstream rowstart = row_base + lo_f - lo_at
-// (hi_run / lo_at = 0 unless the gap is mixed).  A block takes kFR
-// consecutive reads: their flank bytes are contiguous, so the block streams
-// them with coalesced dword loads, flat over bytes.  Rows of the first read's
-// gap (for full-length reads: gap 0 upstream, gap n downstream -- the hot
-// gaps) are tallied in LDS windows, everything else with global atomics.
+// (hi_run / lo_at = 0 unless the gap is mixed).  Each WAVE owns 64
+// consecutive reads (one per lane: its record, its two row starts); their
+// flank bytes are contiguous, so the wave stages them in its LDS with 16-byte
+// loads (both sides before any tally) and walks them in 256-byte segments,
+// consecutive lanes on consecutive bytes.  The owner of a byte needs no block
+// barrier: the lane of a flank starting in the segment marks its start byte
+// in the wave's LDS row, and a max-scan over the segment (a byte's owner is
+// the last flank starting at or before it) gives every byte its flank's lane,
+// whose row offset one ds_bpermute fetches.  Rows of the hot gaps (the
+// block's first reads' gaps: for full-length reads gap 0 upstream, gap n
+// downstream) are tallied in LDS windows, everything else with global
+// atomics.  The only block barriers: window placement (after the first
+// records are loaded) and the flush.
 // ---------------------------------------------------------------------------
-constexpr int kFR = 512;        // reads per block (one per thread): C2's 200k reads fit one round of resident blocks
-constexpr int kFRSmall = 128;   // ... when kFR-read blocks would not give every CU one (C1: 40 -> 157 blocks)
+#ifndef MPC_FLANK_WAVES
+#define MPC_FLANK_WAVES 8
+#endif
+constexpr int kFW = MPC_FLANK_WAVES;  // waves per block (64 reads each): C2's 200k reads fit one round of resident blocks
+constexpr int kFWSmall = 2;     // ... when kFW-wave blocks would not give every CU one (C1)
 constexpr int kWinRows = 256;   // LDS window rows per flank side
+constexpr int kFSeg = 256;      // flank bytes per wave step (4 per lane)
+constexpr int kFStageLd = 2;    // 16-byte loads per lane per staged side (2 KiB per wave)
+constexpr int kFStage = kFStageLd * 1024 - 16;  // flank bytes per side staged per wave (C3: 64 reads x 0-40 B, mean 1280)
+#ifndef MPC_FLANK_BLOCKS_MAX
+#define MPC_FLANK_BLOCKS_MAX (1 << 30)
+#endif
 
 struct FlankArgs {
   uint32_t* status; const int32_t* sample; const int32_t* n_of; const int32_t* gbase;
@@ -2709,219 +2726,184 @@ __device__ __forceinline__ int code_exact(uint32_t c) {
   return c == expect ? code : -1;
 }
 
-constexpr int kStageB = 16384;
-// K_flank per-byte loop: 4 consecutive bytes per thread (1) or one (0)
-#ifndef MPC_FLANK_BYTES4
-#define MPC_FLANK_BYTES4 0
-#endif
-#ifndef MPC_FLANK_BLOCKS_MAX
-#define MPC_FLANK_BLOCKS_MAX (1 << 30)
-#endif  // flank bytes staged in LDS per chunk (a block's range is processed in chunks; C2: 1 per side)
+// gap of read r's flank on one side (-1: empty flank or no row), for the window vote
+__device__ __forceinline__ int32_t flank_gap(const FlankArgs& a, int64_t r, int side) {
+  const int64_t* off = side ? a.down_off : a.up_off;
+  if (off[r + 1] <= off[r]) return -1;
+  const int s = a.sample[r];
+  const int x = side ? a.i_end[r] : a.tstart[r];
+  return (x >= 0 && x <= a.n_of[s]) ? a.gbase[s] + x : -1;
+}
 
-// Byte-parallel: the block's flank bytes (both sides) are staged in LDS chunk by
-// chunk; every thread takes 4 consecutive bytes.  The owner of a byte is found
-// without a search: the starts of the block's non-empty flanks are bits of a
-// chunk bitmap with per-word prefix counts, so owner(x) = (starts <= x) - 1 in
-// the compacted list of non-empty flanks {start, row of byte 0}.
-template <int FR>  // reads per block (one per thread)
-__global__ __launch_bounds__(FR) void K_flank(FlankArgs a) {
+template <int NW>  // waves per block
+__global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
   // row r, code c at word 5 r + c: consecutive rows (the bytes of one flank,
   // on consecutive lanes) fall on distinct banks
   __shared__ uint32_t win[2][kWinRows * 5];
-  __shared__ __attribute__((aligned(16))) uint8_t stage[kStageB + 16];
-  __shared__ int32_t t_start[FR], t_row[FR], t_read[FR];  // compacted non-empty flanks of the current side
-  __shared__ uint32_t bm[kStageB / 32];                      // flank starts in the chunk
-  __shared__ int32_t wpre[kStageB / 32];                     // starts before each bitmap word (+ chunk base)
-  __shared__ int32_t s_gap[2][FR];
+  __shared__ __attribute__((aligned(16))) uint32_t own[NW][kFSeg];  // per wave: 1 + lane of the flank starting at each byte
+  __shared__ __attribute__((aligned(16))) uint8_t stg[NW][2][kFStageLd * 64 * 16];  // per wave and side: staged flank bytes
   __shared__ int64_t s_w0[2];
-  __shared__ int32_t s_w[FR / 64], s_nne, s_cbase;
   if (a.status[MPC_ST_FLAGS] & (DE_CAP | DE_INTERNAL)) return;
-  const int tid = threadIdx.x, l = lane(), w = tid >> 6;
+  const int tid = threadIdx.x, l = lane();
+  const int w = uniform_i32(tid >> 6);
   const int64_t tot = a.status[MPC_ST_ROWS_NEEDED];
   for (int k = tid; k < 2 * kWinRows * 5; k += blockDim.x) (&win[0][0])[k] = 0;
-  uint32_t lerr = 0;
-  int64_t lread = INT64_MAX;
-  // chunks of FR reads, grid-stride: the LDS windows (placed by the block's
-  // first chunk) are flushed once per block, not once per chunk -- the flush
-  // atomics of every block land on the same rows (the hot gaps)
-  const int64_t nchunks = (a.N + FR - 1) / FR;
-#pragma unroll 1
-  for (int64_t ck = blockIdx.x; ck < nchunks; ck += gridDim.x) {
-  const int64_t r0 = ck * FR;
-  const int64_t r1 = r0 + FR < a.N ? r0 + FR : a.N;
-  const int nr = (int)(r1 - r0);
-  const int64_t r = r0 + tid;
-  const bool live = tid < nr;
-  // per-read records: flank byte ranges and the row of byte 0 of each flank
-  int s = 0, ts = 0, ie = 0;
-  int64_t off[2] = {0, 0}, end[2] = {0, 0};
-  if (live) {
-    s = a.sample[r]; ts = a.tstart[r]; ie = a.i_end[r];
-    off[0] = a.up_off[r]; end[0] = a.up_off[r + 1];
-    off[1] = a.down_off[r]; end[1] = a.down_off[r + 1];
-  }
-  int64_t rs[2] = {-1, -1};
-  int32_t gap[2] = {-1, -1};
-  if (live) {
-    const int n = a.n_of[s];
-    const int64_t gb = a.gbase[s];
-    const int64_t ul = end[0] - off[0];
-    if (ul > 0 && ts >= 0 && ts <= n) {  // LEFT at gap tstart: byte j -> row_base + lo_f + hi_run - L + j
-      const int64_t g = gb + ts;
-      int64_t hi = 0;
-      if (a.right_start[g + 1] > a.right_start[g])
-        hi = a.hiR[run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + r)];
-      rs[0] = (int64_t)a.row_base[g] + a.lo_f[g] + hi - ul;
-      gap[0] = (int32_t)g;
-    }
-    const int64_t dl = end[1] - off[1];
-    if (dl > 0 && ie >= 0 && ie <= n) {  // RIGHT at gap i_end: byte j -> row_base + lo_f - lo_at + j
-      const int64_t g = gb + ie;
-      int64_t lo_at = 0;
-      if (a.right_start[g + 1] > a.right_start[g]) {
-        const int64_t t = a.rpos[r];
-        lo_at = a.loR[(int64_t)a.right_start[g] + g + a.roff[g] + (t - a.rsl[g])];
-      }
-      rs[1] = (int64_t)a.row_base[g] + a.lo_f[g] - lo_at;
-      gap[1] = (int32_t)g;
-    }
-  }
-  __syncthreads();  // the previous chunk is done with the shared tables
-  s_gap[0][tid] = gap[0];
-  s_gap[1][tid] = gap[1];
-  __syncthreads();
-  if (tid < 2 && ck == blockIdx.x) {  // LDS window: rows of the gap most of the first chunk's reads use (vote of 3)
-    const int32_t x = s_gap[tid][0], y = s_gap[tid][nr / 2], z = s_gap[tid][nr - 1];
+  constexpr int64_t RB = NW * 64;
+  const int64_t nchunks = (a.N + RB - 1) / RB;
+  if (tid < 2) {  // LDS window: rows of the gap most of the block's first reads use (vote of 3)
+    const int64_t c0 = (int64_t)blockIdx.x * RB;
+    const int64_t nr = a.N - c0 < RB ? a.N - c0 : RB;
+    const int32_t x = flank_gap(a, c0, tid), y = flank_gap(a, c0 + nr / 2, tid), z = flank_gap(a, c0 + nr - 1, tid);
     const int32_t gw = (x == y || x == z) ? x : y;
     s_w0[tid] = gw >= 0 ? (int64_t)a.row_base[gw] : (int64_t)INT32_MIN;
   }
+  uint32_t lerr = 0;
+  int64_t lread = INT64_MAX;
+  uint32_t* ow_w = own[w];
+  bool placed = false;
 #pragma unroll 1
-  for (int side = 0; side < 2; ++side) {
-    const uint8_t* src = side ? a.down : a.up;
-    const int64_t B0 = side ? a.down_off[r0] : a.up_off[r0];
-    const int64_t nb = (side ? a.down_off[r1] : a.up_off[r1]) - B0;  // bytes of the block's flanks
-    // compacted list of non-empty flanks (in read order: starts strictly increase)
-    const int64_t L = end[side] - off[side];
-    const bool ne = live && L > 0;
-    if (ne && (rs[side] >= 0) && rs[side] + L > tot) lerr |= DE_INTERNAL;
-    const int f = ne ? 1 : 0;
-    const int inc = wave_scan_i32(f);
-    __syncthreads();  // previous side / window vote done with the shared tables
-    if (l == 63) s_w[w] = inc;
-    __syncthreads();
-    int wp = 0;
-    for (int k = 0; k < w; ++k) wp += s_w[k];
-    const int c = wp + inc - f;
-    if (ne) {
-      t_start[c] = (int32_t)(off[side] - B0);
-      t_row[c] = (rs[side] >= 0 && rs[side] + L <= tot) ? (int32_t)rs[side] : -1;
-      t_read[c] = tid;
+  for (int64_t ck = blockIdx.x; ck < nchunks; ck += gridDim.x) {
+    const int64_t rb = ck * RB + (int64_t)w * 64;  // the wave's first read
+    const int64_t r = rb + l;
+    const bool live = r < a.N;
+    // per-read records: flank byte ranges and the row of byte 0 of each flank
+    int64_t off[2] = {0, 0}, end[2] = {0, 0}, rs[2] = {-1, -1};
+    if (live) {
+      const int s = a.sample[r], ts = a.tstart[r], ie = a.i_end[r];
+      off[0] = a.up_off[r]; end[0] = a.up_off[r + 1];
+      off[1] = a.down_off[r]; end[1] = a.down_off[r + 1];
+      const int n = a.n_of[s];
+      const int64_t gb = a.gbase[s];
+      const int64_t ul = end[0] - off[0], dl = end[1] - off[1];
+      if (ul > 0 && ts >= 0 && ts <= n) {  // LEFT at gap tstart
+        const int64_t g = gb + ts;
+        int64_t hi = 0;
+        if (a.right_start[g + 1] > a.right_start[g])
+          hi = a.hiR[run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + r)];
+        rs[0] = (int64_t)a.row_base[g] + a.lo_f[g] + hi - ul;
+      }
+      if (dl > 0 && ie >= 0 && ie <= n) {  // RIGHT at gap i_end
+        const int64_t g = gb + ie;
+        int64_t lo_at = 0;
+        if (a.right_start[g + 1] > a.right_start[g]) {
+          const int64_t t = a.rpos[r];
+          lo_at = a.loR[(int64_t)a.right_start[g] + g + a.roff[g] + (t - a.rsl[g])];
+        }
+        rs[1] = (int64_t)a.row_base[g] + a.lo_f[g] - lo_at;
+      }
+#pragma unroll
+      for (int side = 0; side < 2; ++side)
+        if (rs[side] >= 0 && rs[side] + (end[side] - off[side]) > tot) { lerr |= DE_INTERNAL; rs[side] = -1; }
     }
-    if (tid == FR - 1) s_nne = wp + inc;
-    const int64_t w0 = s_w0[side];
-    uint32_t* wn = win[side];
-    for (int64_t c0 = 0; c0 < nb; c0 += kStageB) {  // chunks of the block's byte range
-      const int64_t cn = nb - c0 < kStageB ? nb - c0 : kStageB;
+    if (!placed) {  // windows zeroed and placed (block-uniform: the first trip)
       __syncthreads();
-      // stage [B0 + c0, B0 + c0 + cn) at stage[(B0 + c0) & 15 ...]
-      const int64_t A0 = (B0 + c0) & ~(int64_t)15;
-      const int sh0 = (int)((B0 + c0) - A0);
-      for (int64_t x = 16 * tid; x < sh0 + cn; x += 16 * blockDim.x)
-        *reinterpret_cast<uint4*>(&stage[x]) = *reinterpret_cast<const uint4*>(src + A0 + x);
-      for (int k = tid; k < kStageB / 32; k += blockDim.x) bm[k] = 0;
-      if (tid == 0) {  // owner of the chunk's first byte: last non-empty flank starting <= c0
-        int lo = 0, hi = s_nne - 1;
-        while (lo < hi) {
-          const int mid = (lo + hi + 1) >> 1;
-          if (t_start[mid] <= c0) lo = mid; else hi = mid - 1;
-        }
-        s_cbase = lo;
-      }
-      __syncthreads();
-      if (ne) {
-        const int64_t rel = (off[side] - B0) - c0;
-        if (rel > 0 && rel < cn) atomicOr(&bm[rel >> 5], 1u << (rel & 31));
-      }
-      __syncthreads();
-      {  // per-word prefix of the start bits (block scan, WPT consecutive words per thread)
-        constexpr int WPT = (kStageB / 32 + FR - 1) / FR;
-        const int nwd = (int)((cn + 31) >> 5);
-        int c4[WPT], cnt = 0;
+      placed = true;
+    }
+    if (rb >= a.N) continue;
+    const int last = a.N - 1 - rb < 63 ? (int)(a.N - 1 - rb) : 63;  // the wave's last read
+    // the wave's flank bytes of both sides: [Bw, Bw + nb)
+    const int64_t Bw0 = readlane64(off[0], 0), nb0 = readlane64(end[0], last) - Bw0;
+    const int64_t Bw1 = readlane64(off[1], 0), nb1 = readlane64(end[1], last) - Bw1;
+    // stage [Bw + c0, Bw + c0 + kFStage) of a side in the wave's LDS (16-byte
+    // loads from the aligned-down start).  The first stage of BOTH sides is
+    // loaded before any tally: a load issued after a global atomic waits for
+    // that atomic too (vmcnt retires in order), so loads between the atomics
+    // serialized the wave on them)
+    auto stage_load = [&](const uint8_t* src, int64_t B, int64_t nb, int64_t c0, uint4 (&v)[kFStageLd]) {
+      const int64_t A = (B + c0) & ~(int64_t)15;
+      const int64_t cnt = nb - c0 < kFStage ? nb - c0 : kFStage;
+      const int n16 = (int)(((B + c0 - A) + cnt + 15) >> 4);
 #pragma unroll
-        for (int j = 0; j < WPT; ++j) {
-          const int wi = tid * WPT + j;
-          c4[j] = wi < nwd ? __popc(bm[wi]) : 0;
-          cnt += c4[j];
-        }
-        const int i2 = wave_scan_i32(cnt);
-        if (l == 63) s_w[w] = i2;
-        __syncthreads();
-        int run = s_cbase + i2 - cnt;
-        for (int k = 0; k < w; ++k) run += s_w[k];
+      for (int j = 0; j < kFStageLd; ++j)
+        v[j] = l + 64 * j < n16 ? *reinterpret_cast<const uint4*>(src + A + 16 * (l + 64 * j)) : make_uint4(0u, 0u, 0u, 0u);
+    };
+    auto stage_store = [&](uint8_t* st, const uint4 (&v)[kFStageLd]) {
 #pragma unroll
-        for (int j = 0; j < WPT; ++j) {
-          const int wi = tid * WPT + j;
-          if (wi < nwd) wpre[wi] = run;
-          run += c4[j];
-        }
-      }
-      __syncthreads();
-#if MPC_FLANK_BYTES4
-      // every thread takes 4 consecutive bytes (one owner lookup, one stage
-      // dword); consecutive lanes, consecutive dwords: a flank's bytes go to
-      // consecutive rows, so a wave's (rare) global atomics cover a few
-      // contiguous segments instead of one scattered row per lane
-      // 32-bit: rows < row_cap < 2^31, a block's flank bytes < 2^31
-      const int cn32 = (int)cn, c032 = (int)c0;
-      const int32_t w032 = w0 >= 0 ? (int32_t)w0 : -(1 << 30);  // no window: never a hit
-      const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
-      for (int x4 = 4 * tid; x4 < cn32; x4 += 4 * (int)blockDim.x) {
-        const uint32_t word = bm[x4 >> 5];  // (the 4 bytes share a bitmap word)
-        const int ob = wpre[x4 >> 5];
-        const int q = x4 + sh0;             // stage offset (+16 padding: the second dword is in bounds)
-        const uint32_t by = __builtin_amdgcn_alignbyte(s32[(q >> 2) + 1], s32[q >> 2], (uint32_t)(q & 3));
-        int o_prev = -1;
-        int32_t rw = -1, ts = 0;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const int x = x4 + k;
-          if (x >= cn32) break;
-          const int o = ob + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
-          if (o != o_prev) { rw = t_row[o]; ts = t_start[o]; o_prev = o; }
-          if (rw < 0) continue;
-          const int32_t row = rw + (c032 + x - ts);
-          const int code = code_exact((by >> (8 * k)) & 0xffu);
-          if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
+      for (int j = 0; j < kFStageLd; ++j) *reinterpret_cast<uint4*>(st + 16 * (l + 64 * j)) = v[j];
+    };
+    {
+      uint4 v0[kFStageLd], v1[kFStageLd];
+      if (nb0 > 0) stage_load(a.up, Bw0, nb0, 0, v0);
+      if (nb1 > 0) stage_load(a.down, Bw1, nb1, 0, v1);
+      if (nb0 > 0) stage_store(stg[w][0], v0);
+      if (nb1 > 0) stage_store(stg[w][1], v1);
+    }
+#pragma unroll 1
+    for (int side = 0; side < 2; ++side) {
+      const uint8_t* src = side ? a.down : a.up;
+      // (selects, not off[side]: a runtime index would put the arrays in scratch)
+      const int64_t fo = side ? off[1] : off[0], fe = side ? end[1] : end[0], frs = side ? rs[1] : rs[0];
+      const int64_t Bw = side ? Bw1 : Bw0, nb = side ? nb1 : nb0;
+      if (nb <= 0) continue;
+      const int64_t L = fe - fo;
+      const int32_t w032 = s_w0[side] >= 0 ? (int32_t)s_w0[side] : -(1 << 30);  // no window: never a hit
+      uint32_t* wn = win[side];
+      uint8_t* st = stg[w][side];
+      if (nb >= (1 << 30)) {  // (huge flanks: every lane walks its own; rows < 2^31)
+        for (int64_t j = 0; live && frs >= 0 && j < L; ++j) {
+          const int code = code_exact(src[fo + j]);
+          if (code < 0) { lerr |= DE_KEY; lread = r < lread ? r : lread; continue; }
+          const int32_t row = (int32_t)(frs + j);
           const uint32_t wr = (uint32_t)(row - w032);
           if (wr < (uint32_t)kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
           else atomicAdd(a.rows + (int64_t)row * 4 + code, 1u);
         }
+        continue;
+      }
+      // wave-relative byte x of lane l's flank: row = x + rowoff (rs + L <= tot < 2^31;
+      // no row: rowoff = INT32_MIN, so every row of the flank is negative)
+      const int xo = live ? (int)(fo - Bw) : (int)nb;
+      const int32_t rowoff = (live && frs >= 0) ? (int32_t)(frs - xo) : INT32_MIN;
+      const bool ne = live && L > 0;
+      const int nb32 = (int)nb;
+      int carry = 0;  // owner (1 + lane) of the previous byte group's last byte
+#pragma unroll 1
+      for (int c0 = 0; c0 < nb32; c0 += kFStage) {
+        if (c0 > 0) {  // (a wave with more than kFStage bytes on this side)
+          uint4 v[kFStageLd];
+          stage_load(src, Bw, nb, c0, v);
+          stage_store(st, v);
+        }
+        wave_sync_lds();
+        const int sh = (int)((Bw + c0) & 15);
+        const int c1 = nb32 - c0 < kFStage ? nb32 : c0 + kFStage;
+#pragma unroll 1
+        for (int S = c0; S < c1; S += kFSeg) {
+          // lane l takes bytes S + 64 k + l (k < 4): consecutive lanes on
+          // consecutive bytes, so a flank's bytes (consecutive rows) leave as few
+          // 64-B atomic requests as they can (4 bytes per lane put every lane's
+          // row atomic in a segment of its own: C3 K_flank +30 %)
+          *reinterpret_cast<uint4*>(ow_w + 4 * l) = make_uint4(0u, 0u, 0u, 0u);
+          wave_sync_lds();
+          // non-empty flanks start on distinct bytes
+          if (ne && xo >= S && xo < S + kFSeg) ow_w[xo - S] = (uint32_t)(l + 1);
+          wave_sync_lds();
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int x = S + 64 * k + l;
+            const int inc = max(wave_scan_max_i32((int)ow_w[64 * k + l]), carry);
+            carry = wave_last_i32(inc);
+            // the row offset of the byte's flank (owner 0: bytes past the wave's range)
+            const int32_t q = __builtin_amdgcn_ds_bpermute(4 * max(inc - 1, 0), rowoff);
+            if (x >= c1 || inc == 0) continue;
+            const int32_t row = x + q;
+            if (row < 0) continue;  // flank without a row
+            const int code = code_exact(st[sh + (x - c0)]);
+            if (code < 0) {
+              lerr |= DE_KEY;
+              const int64_t rr = rb + inc - 1;
+              lread = rr < lread ? rr : lread;
+              continue;
+            }
+            const uint32_t wr = (uint32_t)(row - w032);
+            if (wr < (uint32_t)kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
+            else atomicAdd(a.rows + (int64_t)row * 4 + code, 1u);
+          }
+        }
+        wave_sync_lds();  // (the stage is reloaded for the next kFStage bytes)
       }
     }
   }
-#else
-      // consecutive lanes take consecutive bytes: a flank's bytes go to
-      // consecutive rows, so a wave's (rare) global atomics cover a few
-      // contiguous segments instead of one scattered row per lane
-      // 32-bit: rows < row_cap < 2^31, a block's flank bytes < 2^31
-      const int cn32 = (int)cn, c032 = (int)c0;
-      const int32_t w032 = w0 >= 0 ? (int32_t)w0 : -(1 << 30);  // no window: never a hit
-      for (int x = tid; x < cn32; x += blockDim.x) {
-        const uint32_t word = bm[x >> 5];
-        const int o = wpre[x >> 5] + __popc(word & (0xffffffffu >> (31 - (x & 31))));  // owner: starts <= x
-        const int32_t rw = t_row[o];
-        if (rw < 0) continue;
-        const int32_t row = rw + (c032 + x - t_start[o]);
-        const int code = code_exact(stage[x + sh0]);
-        if (code < 0) { lerr |= DE_KEY; const int64_t rr = r0 + t_read[o]; lread = rr < lread ? rr : lread; continue; }
-        const uint32_t wr = (uint32_t)(row - w032);
-        if (wr < (uint32_t)kWinRows) atomicAdd(wn + wr * 5 + code, 1u);
-        else atomicAdd(a.rows + (int64_t)row * 4 + code, 1u);
-      }
-    }
-  }
-#endif
-  }  // chunks
   __syncthreads();
   for (int side = 0; side < 2; ++side) {
     const int64_t w0 = s_w0[side];
@@ -3324,12 +3306,11 @@ static void launch_left(const mpc_plan* p, const Dev& d, hipStream_t st) {
   else hipLaunchKernelGGL(K_left<kUB>, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));
 }
 static int64_t ins_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 512)); }
-static int flank_reads(const mpc_plan* p) { return (p->N + kFR - 1) / kFR < 256 ? kFRSmall : kFR; }
-// K_flank blocks: chunks of flank_reads reads, at most about four resident
-// blocks per CU (each further chunk of a block shares its window flush)
+static int flank_waves(const mpc_plan* p) { return (p->N + kFW * 64 - 1) / (kFW * 64) < 256 ? kFWSmall : kFW; }
+// K_flank blocks: one per chunk of flank_waves * 64 reads, unless capped
 constexpr int64_t kFlankBlocksMax = MPC_FLANK_BLOCKS_MAX;
 static int64_t flank_grid(const mpc_plan* p) {
-  const int fr = flank_reads(p);
+  const int64_t fr = flank_waves(p) * 64;
   return std::max<int64_t>(1, std::min<int64_t>(kFlankBlocksMax, (p->N + fr - 1) / fr));
 }
 
@@ -3356,10 +3337,10 @@ static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
   return a;
 }
 static void launch_flank(const mpc_plan* p, const Dev& d, hipStream_t st) {
-  if (flank_reads(p) == kFRSmall)
-    hipLaunchKernelGGL(K_flank<kFRSmall>, dim3(flank_grid(p)), dim3(kFRSmall), 0, st, flank_args(p, d));
+  if (flank_waves(p) == kFWSmall)
+    hipLaunchKernelGGL(K_flank<kFWSmall>, dim3(flank_grid(p)), dim3(kFWSmall * 64), 0, st, flank_args(p, d));
   else
-    hipLaunchKernelGGL(K_flank<kFR>, dim3(flank_grid(p)), dim3(kFR), 0, st, flank_args(p, d));
+    hipLaunchKernelGGL(K_flank<kFW>, dim3(flank_grid(p)), dim3(kFW * 64), 0, st, flank_args(p, d));
 }
 
 // One launch clears every accumulator of a run (status, bitmaps, tallies, rows).

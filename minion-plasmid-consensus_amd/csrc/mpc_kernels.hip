@@ -2386,7 +2386,10 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       // the bases too, run-relative (LEFT: base bi from the 3' end lands on the
       // run's slot hi_run - 1 - bi, :37-62): K_ins maps them to rows after the layout
       if (k < kKMax) {
-        atomicMax(&Ml[p * kMs + k], (uint32_t)L);
+        // the run's longest LEFT string: UB = 1024 takes it from the highest
+        // slot holding a base at the flush (one LDS atomic less per event: C4
+        // K_left 230 -> 220 us); UB = 512 (C5: +5 us that way) per event
+        if constexpr (kLean) atomicMax(&Ml[p * kMs + k], (uint32_t)L);
         uint32_t* tp = Tl + p * kTs + k * 16;
 #pragma unroll
         for (int j = 0; j < kInsInline; ++j)  // straight-line: bases j < L
@@ -2422,15 +2425,19 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       MPC_LSEG(6);
       continue;
     }
+    for (int q = threadIdx.x; q < kBW * kKMax * 16; q += blockDim.x) {  // contiguous per (gap, run)
+      const int k = (q >> 4) % kKMax, p = (q >> 4) / kKMax;
+      const uint32_t v = Tl[p * kTs + k * 16 + (q & 15)];
+      if (v) {
+        atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + k) * 16 + (q & 15), v);
+        atomicMax(&Ml[p * kMs + k], (uint32_t)((q & 15) >> 2) + 1u);  // slot bi holds a base: M > bi
+      }
+    }
+    __syncthreads();
     for (int q = threadIdx.x; q < kBW * kKMax; q += blockDim.x) {
       const int k = q % kKMax, p = q / kKMax;
       const uint32_t m = Ml[p * kMs + k];
       if (m) atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + k, (int32_t)m);
-    }
-    for (int q = threadIdx.x; q < kBW * kKMax * 16; q += blockDim.x) {  // contiguous per (gap, run)
-      const int k = (q >> 4) % kKMax, p = (q >> 4) / kKMax;
-      const uint32_t v = Tl[p * kTs + k * 16 + (q & 15)];
-      if (v) atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + k) * 16 + (q & 15), v);
     }
     __syncthreads();
     MPC_LSEG(6);
@@ -2875,8 +2882,10 @@ __global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
           // row atomic in a segment of its own: C3 K_flank +30 %)
           *reinterpret_cast<uint4*>(ow_w + 4 * l) = make_uint4(0u, 0u, 0u, 0u);
           wave_sync_lds();
-          // non-empty flanks start on distinct bytes
-          if (ne && xo >= S && xo < S + kFSeg) ow_w[xo - S] = (uint32_t)(l + 1);
+          // non-empty flanks start on distinct bytes; only starts in this
+          // stage (< c1): a later one would enter the carry into the next
+          // stage ahead of the bytes before it
+          if (ne && xo >= S && xo < S + kFSeg && xo < c1) ow_w[xo - S] = (uint32_t)(l + 1);
           wave_sync_lds();
 #pragma unroll
           for (int k = 0; k < 4; ++k) {
@@ -2951,36 +2960,44 @@ __device__ __forceinline__ int sample_of_row_lds(const Dev& d, const int32_t* sr
 constexpr int kCRBig = 8;
 constexpr int64_t kCallBlocksMax = 512;  // (the 70 kb parity case takes the kCRBig path)
 
-// per slot: sorted(tuples in dict order, key=count)[::-1] -> top / second / tie -> N (:363-423)
+// per slot: sorted(tuples in dict order, key=count)[::-1] -> top / second / tie -> N (:363-423).
+// The stable descending sort of the reverse-dict-ordered (base, count) list
+// is a descending sort of the keys count << 2 | dict index; bases with count
+// 0 are not in the list (they sort last, and no positive count ties them).
+// Branch-free: a 5-exchange sorting network (no register-indexed arrays: the
+// insertion sort put them in scratch, K_call<8> spilled 18 VGPRs).
 __device__ __forceinline__ uint4 call_slot(uint4 cv, double gtf, uint32_t* total_out) {
-  const uint32_t c[4] = {cv.x, cv.y, cv.z, cv.w};  // A, T, C, G
-  const uint32_t total = c[0] + c[1] + c[2] + c[3];
+  const uint32_t total = cv.x + cv.y + cv.z + cv.w;  // A, T, C, G
   *total_out = total;
   if (total == 0) return make_uint4(0, 0, 0, 0);
-  // descending count, ties in reverse dict order (stable sort then reverse, :371-374)
-  int idx[4], m = 0;
-  for (int k = 3; k >= 0; --k) if (c[k] > 0) idx[m++] = k;   // reverse dict order
-  for (int a = 1; a < m; ++a) {                               // stable sort descending
-    const int t = idx[a];
-    int b = a - 1;
-    while (b >= 0 && c[idx[b]] < c[t]) { idx[b + 1] = idx[b]; --b; }
-    idx[b + 1] = t;
-  }
-  const char names[4] = {'A', 'T', 'C', 'G'};
-  uint32_t base, base2, count, count2;
-  if (m == 1 || c[idx[0]] > c[idx[1]]) { base = names[idx[0]]; count = c[idx[0]]; }
-  else { base = 'N'; count = 0; for (int a = 0; a < m; ++a) if (c[idx[a]] == c[idx[0]]) count += c[idx[a]]; }
-  if (m <= 1) { base2 = 'X'; count2 = 0; }
-  else if (m == 2 || c[idx[1]] > c[idx[2]]) { base2 = names[idx[1]]; count2 = c[idx[1]]; }
-  else { base2 = 'N'; count2 = 0; for (int a = 0; a < m; ++a) if (c[idx[a]] == c[idx[1]]) count2 += c[idx[a]]; }
+  uint64_t k0 = ((uint64_t)cv.x << 2) | 0u, k1 = ((uint64_t)cv.y << 2) | 1u;
+  uint64_t k2 = ((uint64_t)cv.z << 2) | 2u, k3 = ((uint64_t)cv.w << 2) | 3u;
+  auto cx = [](uint64_t& a, uint64_t& b) {  // a >= b after
+    const uint64_t hi = a > b ? a : b, lo = a > b ? b : a;
+    a = hi; b = lo;
+  };
+  cx(k0, k1); cx(k2, k3); cx(k0, k2); cx(k1, k3); cx(k1, k2);
+  const uint32_t c0 = (uint32_t)(k0 >> 2), c1 = (uint32_t)(k1 >> 2), c2 = (uint32_t)(k2 >> 2), c3 = (uint32_t)(k3 >> 2);
+  // 'A' 'T' 'C' 'G' by dict index
+  auto name = [](uint64_t k) -> uint32_t { return (0x47435441u >> (8 * (uint32_t)(k & 3u))) & 0xffu; };
+  const uint32_t m = (c0 > 0) + (c1 > 0) + (c2 > 0) + (c3 > 0);  // c0 > 0 (total > 0)
+  // ties of the first / second count (every tied count is positive: c0 > 0, and c1 is tested only when m >= 2)
+  const uint32_t tie0 = c0 * (1u + (c1 == c0) + (c2 == c0) + (c3 == c0));
+  const uint32_t tie1 = c1 * ((c0 == c1) + 1u + (c2 == c1) + (c3 == c1));
+  const bool one = m == 1 || c0 > c1;
+  uint32_t base = one ? name(k0) : 'N';
+  const uint32_t count = one ? c0 : tie0;
+  const bool two = m == 2 || c1 > c2;
+  const uint32_t base2 = m <= 1 ? 'X' : (two ? name(k1) : 'N');
+  const uint32_t count2 = m <= 1 ? 0u : (two ? c1 : tie1);
   const uint32_t chrom1 = base;
   if ((double)count < gtf * (double)count2) base = 'N';   // :421
   return make_uint4(base | (chrom1 << 8) | (base2 << 16) | (1u << 24), count, count2, total);
 }
 
 // calls of every row + max depth over slot 0 (:332-341); rows t + 256 k of the block
-template <int kCR>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(8))) void K_call(Dev d, int64_t R) {
+template <int kCR>  // (kCR rows in flight per thread: up to 128 VGPRs, no spills)
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(kCR > 1 ? 4 : 8))) void K_call(Dev d, int64_t R) {
   constexpr int kCB = 256 * kCR;  // rows per block
   __shared__ int32_t srow[kSmpLds];
   __shared__ int32_t s_blk[2], s_w[4];

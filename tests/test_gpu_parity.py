@@ -123,6 +123,9 @@ SYNTH = [
     dict(n=50, n_reads=2000, profile="c1probe", seed=7, frac_partial=0.5, flank=(0, 8)),
     dict(n=3000, n_reads=500, profile="default", seed=9, frac_partial=0.3, ins_len=(1, 1500), del_len=(1, 1200),
          p_ins=0.0005, p_del=0.0005, flank=(0, 3000)),
+    # K_flank: 64 reads' flanks around its 2032-byte per-wave stage (some waves
+    # one stage, some two: the owner carry across the stage boundary)
+    dict(n=900, n_reads=6000, profile="indel", seed=73, frac_partial=0.5, flank=(0, 64)),
     # every K_parse tally mode the planner uses (tests/geometry_util.py): the
     # shortest reference in each LDS mode, mode 3 also with 3 substitution
     # windows (> 2 x 16384 positions), and the global-atomic mode 0

@@ -2710,8 +2710,10 @@ constexpr int kWinRows = 256;   // LDS window rows per flank side
 constexpr int kFSeg = 256;      // flank bytes per wave step (4 per lane)
 constexpr int kFStageLd = 2;    // 16-byte loads per lane per staged side (2 KiB per wave)
 constexpr int kFStage = kFStageLd * 1024 - 16;  // flank bytes per side staged per wave (C3: 64 reads x 0-40 B, mean 1280)
+// K_flank blocks at most (two per CU): beyond, a block takes a contiguous range of
+// chunks (C3: 1954 one-chunk blocks 135 us, 512 blocks of ~4 chunks 110 us)
 #ifndef MPC_FLANK_BLOCKS_MAX
-#define MPC_FLANK_BLOCKS_MAX (1 << 30)
+#define MPC_FLANK_BLOCKS_MAX 512
 #endif
 
 struct FlankArgs {
@@ -2742,34 +2744,50 @@ __device__ __forceinline__ int32_t flank_gap(const FlankArgs& a, int64_t r, int 
   return (x >= 0 && x <= a.n_of[s]) ? a.gbase[s] + x : -1;
 }
 
-template <int NW>  // waves per block
+template <int NW, bool MULTI>  // waves per block; blocks take several chunks (grid capped)
 __global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
   // row r, code c at word 5 r + c: consecutive rows (the bytes of one flank,
   // on consecutive lanes) fall on distinct banks
   __shared__ uint32_t win[2][kWinRows * 5];
   __shared__ __attribute__((aligned(16))) uint32_t own[NW][kFSeg];  // per wave: 1 + lane of the flank starting at each byte
   __shared__ __attribute__((aligned(16))) uint8_t stg[NW][2][kFStageLd * 64 * 16];  // per wave and side: staged flank bytes
-  __shared__ int64_t s_w0[2];
+  // the windows' first rows: placed, and voted for the chunk (by chunk parity: a
+  // wave still comparing chunk k's vote never sees chunk k + 1's)
+  __shared__ int64_t s_w0[2], s_wn[2][2];
   if (a.status[MPC_ST_FLAGS] & (DE_CAP | DE_INTERNAL)) return;
   const int tid = threadIdx.x, l = lane();
   const int w = uniform_i32(tid >> 6);
   const int64_t tot = a.status[MPC_ST_ROWS_NEEDED];
-  for (int k = tid; k < 2 * kWinRows * 5; k += blockDim.x) (&win[0][0])[k] = 0;
   constexpr int64_t RB = NW * 64;
+  for (int k = tid; k < 2 * kWinRows * 5; k += blockDim.x) (&win[0][0])[k] = 0;
   const int64_t nchunks = (a.N + RB - 1) / RB;
-  if (tid < 2) {  // LDS window: rows of the gap most of the block's first reads use (vote of 3)
-    const int64_t c0 = (int64_t)blockIdx.x * RB;
-    const int64_t nr = a.N - c0 < RB ? a.N - c0 : RB;
-    const int32_t x = flank_gap(a, c0, tid), y = flank_gap(a, c0 + nr / 2, tid), z = flank_gap(a, c0 + nr - 1, tid);
-    const int32_t gw = (x == y || x == z) ? x : y;
-    s_w0[tid] = gw >= 0 ? (int64_t)a.row_base[gw] : (int64_t)INT32_MIN;
-  }
+  // the block's chunks: a contiguous range (one sample's reads but at sample
+  // boundaries), so its windows are flushed once per range, not per chunk --
+  // every block's flush adds into the same hot rows (C3: 1954 one-chunk blocks)
+  const int64_t cpb = MULTI ? (nchunks + gridDim.x - 1) / gridDim.x : 1;
+  const int64_t ck0 = (int64_t)blockIdx.x * cpb, ck1 = ck0 + cpb < nchunks ? ck0 + cpb : nchunks;
+  auto flush = [&]() {
+    for (int side = 0; side < 2; ++side) {
+      const int64_t w0 = s_w0[side];
+      for (int k = tid; k < kWinRows * 4; k += blockDim.x) {
+        const uint32_t v = win[side][(k >> 2) * 5 + (k & 3)];
+        if (v) atomicAdd(a.rows + w0 * 4 + k, v);
+      }
+    }
+  };
   uint32_t lerr = 0;
   int64_t lread = INT64_MAX;
   uint32_t* ow_w = own[w];
-  bool placed = false;
 #pragma unroll 1
-  for (int64_t ck = blockIdx.x; ck < nchunks; ck += gridDim.x) {
+  for (int64_t ck = ck0; ck < ck1; ++ck) {
+    if (tid < 2) {  // LDS window: rows of the gap most of the chunk's reads use (vote of 3)
+      const int64_t c0 = ck * RB;
+      const int64_t nr = a.N - c0 < RB ? a.N - c0 : RB;
+      const int32_t x = flank_gap(a, c0, tid), y = flank_gap(a, c0 + nr / 2, tid), z = flank_gap(a, c0 + nr - 1, tid);
+      const int32_t gw = (x == y || x == z) ? x : y;
+      s_wn[ck & 1][tid] = gw >= 0 ? (int64_t)a.row_base[gw] : (int64_t)INT32_MIN;
+      if (ck == ck0) s_w0[tid] = s_wn[ck & 1][tid];  // the first placement (windows zeroed above)
+    }
     const int64_t rb = ck * RB + (int64_t)w * 64;  // the wave's first read
     const int64_t r = rb + l;
     const bool live = r < a.N;
@@ -2802,9 +2820,14 @@ __global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
       for (int side = 0; side < 2; ++side)
         if (rs[side] >= 0 && rs[side] + (end[side] - off[side]) > tot) { lerr |= DE_INTERNAL; rs[side] = -1; }
     }
-    if (!placed) {  // windows zeroed and placed (block-uniform: the first trip)
+    __syncthreads();  // the vote is in; every wave is done with the previous chunk
+    const int64_t* wn_ = s_wn[ck & 1];
+    if (MULTI && (wn_[0] != s_w0[0] || wn_[1] != s_w0[1])) {  // (block-uniform) windows move: flush, clear, place
+      flush();
       __syncthreads();
-      placed = true;
+      for (int k = tid; k < 2 * kWinRows * 5; k += blockDim.x) (&win[0][0])[k] = 0;
+      if (tid < 2) s_w0[tid] = wn_[tid];
+      __syncthreads();
     }
     if (rb >= a.N) continue;
     const int last = a.N - 1 - rb < 63 ? (int)(a.N - 1 - rb) : 63;  // the wave's last read
@@ -2914,13 +2937,7 @@ __global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
     }
   }
   __syncthreads();
-  for (int side = 0; side < 2; ++side) {
-    const int64_t w0 = s_w0[side];
-    for (int k = tid; k < kWinRows * 4; k += blockDim.x) {
-      const uint32_t v = win[side][(k >> 2) * 5 + (k & 3)];
-      if (v) atomicAdd(a.rows + w0 * 4 + k, v);
-    }
-  }
+  if (ck1 > ck0) flush();
   if (lerr) {
     atomicOr(&a.status[MPC_ST_FLAGS], lerr);
     if (lread != INT64_MAX) atomicMin(&a.status[MPC_ST_FIRST_READ], (uint32_t)lread);
@@ -3324,7 +3341,7 @@ static void launch_left(const mpc_plan* p, const Dev& d, hipStream_t st) {
 }
 static int64_t ins_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 512)); }
 static int flank_waves(const mpc_plan* p) { return (p->N + kFW * 64 - 1) / (kFW * 64) < 256 ? kFWSmall : kFW; }
-// K_flank blocks: one per chunk of flank_waves * 64 reads, unless capped
+// K_flank blocks: one per chunk of flank_waves * 64 reads, at most kFlankBlocksMax
 constexpr int64_t kFlankBlocksMax = MPC_FLANK_BLOCKS_MAX;
 static int64_t flank_grid(const mpc_plan* p) {
   const int64_t fr = flank_waves(p) * 64;
@@ -3354,10 +3371,17 @@ static FlankArgs flank_args(const mpc_plan* p, const Dev& d) {
   return a;
 }
 static void launch_flank(const mpc_plan* p, const Dev& d, hipStream_t st) {
-  if (flank_waves(p) == kFWSmall)
-    hipLaunchKernelGGL(K_flank<kFWSmall>, dim3(flank_grid(p)), dim3(kFWSmall * 64), 0, st, flank_args(p, d));
-  else
-    hipLaunchKernelGGL(K_flank<kFW>, dim3(flank_grid(p)), dim3(kFW * 64), 0, st, flank_args(p, d));
+  const int nw = flank_waves(p);
+  const dim3 grid((unsigned)flank_grid(p)), block((unsigned)(nw * 64));
+  const bool multi = flank_grid(p) < (p->N + nw * 64 - 1) / (nw * 64);  // blocks take chunk ranges
+  const FlankArgs fa = flank_args(p, d);
+  if (nw == kFWSmall) {
+    if (multi) hipLaunchKernelGGL((K_flank<kFWSmall, true>), grid, block, 0, st, fa);
+    else hipLaunchKernelGGL((K_flank<kFWSmall, false>), grid, block, 0, st, fa);
+  } else {
+    if (multi) hipLaunchKernelGGL((K_flank<kFW, true>), grid, block, 0, st, fa);
+    else hipLaunchKernelGGL((K_flank<kFW, false>), grid, block, 0, st, fa);
+  }
 }
 
 // One launch clears every accumulator of a run (status, bitmaps, tallies, rows).

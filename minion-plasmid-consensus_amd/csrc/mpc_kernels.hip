@@ -7,8 +7,10 @@
 //   parse     K_clear        zero the per-launch state
 //             K_parse        per workgroup: contiguous reads of one sample.  cs
 //                            ':'+op units -> substitution / deletion / span
-//                            tallies (LDS), insertion events (bucket-sorted by
-//                            gap), i_end, LEFT-event gap bitmap, error flags
+//                            tallies (LDS), insertion events (64-event pages
+//                            per 64-gap bucket, written once), i_end, LEFT-event
+//                            gap bitmap, error flags
+//             K_subs/K_subsum tally mode 3: substitution events -> tallies
 //   index     K_rsplit_units RIGHT events: mixed gaps -> sort keys, RIGHT-only
 //                            gaps -> longest flank; insertion work units
 //             K_rsort        stable (gap, read) order of the mixed RIGHT events
@@ -801,10 +803,10 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, uint3
 // processed ONE UNIT PER LANE, 64 per round: branch-free SWAR decode of the
 // operand words, one DPP scan of the advances for the coordinates i (reads
 // are segments: per-read bases in a slot table), ballot/mbcnt for the read
-// slot and the insertion event index.  Effects: substitution / deletion / span tallies (LDS, 12 B per
-// position), insertion events (stored straight into the wave's region of
-// ins_raw), LEFT-gap bits (LDS bitmap).  Epilogue: flush tallies, bucket-sort
-// the insertion events by gap.
+// slot.  Effects: substitution / deletion / span tallies (LDS in tally modes
+// 1-3), insertion events placed once into 64-event pages of their (workgroup,
+// bucket) (parse_place_event), LEFT-gap bits (LDS bitmap).  Epilogue: flush
+// the tallies, list every bucket's pages (parse_epilogue).
 template <int TM, int WIN>
 __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   constexpr int CH = WIN / 64;

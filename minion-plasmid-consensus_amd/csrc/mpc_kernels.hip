@@ -2747,7 +2747,7 @@ __device__ __forceinline__ int32_t flank_gap(const FlankArgs& a, int64_t r, int 
 }
 
 template <int NW, bool MULTI>  // waves per block; blocks take several chunks (grid capped)
-__global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MULTI ? 4 : 6))) void K_flank(FlankArgs a) {
   // row r, code c at word 5 r + c: consecutive rows (the bytes of one flank,
   // on consecutive lanes) fall on distinct banks
   __shared__ uint32_t win[2][kWinRows * 5];
@@ -2793,21 +2793,28 @@ __global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
     const int64_t rb = ck * RB + (int64_t)w * 64;  // the wave's first read
     const int64_t r = rb + l;
     const bool live = r < a.N;
-    // per-read records: flank byte ranges and the row of byte 0 of each flank
-    int64_t off[2] = {0, 0}, end[2] = {0, 0}, rs[2] = {-1, -1};
+    // per-read records: flank byte ranges and the row of byte 0 of each flank,
+    // kept in 32 bits past this point (rows < 2^31; a flank longer than 2^31 - 1
+    // bytes takes the HBM path below with its 64-bit offsets reloaded): fewer
+    // VGPRs, more resident waves -- the other batches' kernels in flight get
+    // the CUs K_flank does not hold
+    int64_t off0 = 0, off1 = 0;
+    int32_t L0 = 0, L1 = 0, rw0 = -1, rw1 = -1;
     if (live) {
       const int s = a.sample[r], ts = a.tstart[r], ie = a.i_end[r];
-      off[0] = a.up_off[r]; end[0] = a.up_off[r + 1];
-      off[1] = a.down_off[r]; end[1] = a.down_off[r + 1];
+      off0 = a.up_off[r];
+      off1 = a.down_off[r];
+      const int64_t ul = a.up_off[r + 1] - off0, dl = a.down_off[r + 1] - off1;
       const int n = a.n_of[s];
       const int64_t gb = a.gbase[s];
-      const int64_t ul = end[0] - off[0], dl = end[1] - off[1];
       if (ul > 0 && ts >= 0 && ts <= n) {  // LEFT at gap tstart
         const int64_t g = gb + ts;
         int64_t hi = 0;
         if (a.right_start[g + 1] > a.right_start[g])
           hi = a.hiR[run_left(a.right_start, a.rsl, a.roff, a.vals_out, g, a.read_offset + r)];
-        rs[0] = (int64_t)a.row_base[g] + a.lo_f[g] + hi - ul;
+        const int64_t rs = (int64_t)a.row_base[g] + a.lo_f[g] + hi - ul;
+        if (rs >= 0 && rs + ul > tot) lerr |= DE_INTERNAL;
+        else rw0 = (int32_t)rs;
       }
       if (dl > 0 && ie >= 0 && ie <= n) {  // RIGHT at gap i_end
         const int64_t g = gb + ie;
@@ -2816,11 +2823,12 @@ __global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
           const int64_t t = a.rpos[r];
           lo_at = a.loR[(int64_t)a.right_start[g] + g + a.roff[g] + (t - a.rsl[g])];
         }
-        rs[1] = (int64_t)a.row_base[g] + a.lo_f[g] - lo_at;
+        const int64_t rs = (int64_t)a.row_base[g] + a.lo_f[g] - lo_at;
+        if (rs >= 0 && rs + dl > tot) lerr |= DE_INTERNAL;
+        else rw1 = (int32_t)rs;
       }
-#pragma unroll
-      for (int side = 0; side < 2; ++side)
-        if (rs[side] >= 0 && rs[side] + (end[side] - off[side]) > tot) { lerr |= DE_INTERNAL; rs[side] = -1; }
+      L0 = ul < INT32_MAX ? (int32_t)ul : INT32_MAX;
+      L1 = dl < INT32_MAX ? (int32_t)dl : INT32_MAX;
     }
     __syncthreads();  // the vote is in; every wave is done with the previous chunk
     const int64_t* wn_ = s_wn[ck & 1];
@@ -2834,8 +2842,11 @@ __global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
     if (rb >= a.N) continue;
     const int last = a.N - 1 - rb < 63 ? (int)(a.N - 1 - rb) : 63;  // the wave's last read
     // the wave's flank bytes of both sides: [Bw, Bw + nb)
-    const int64_t Bw0 = readlane64(off[0], 0), nb0 = readlane64(end[0], last) - Bw0;
-    const int64_t Bw1 = readlane64(off[1], 0), nb1 = readlane64(end[1], last) - Bw1;
+    const int64_t Bw0 = readlane64(off0, 0), nb0 = readlane64(off0 + L0, last) - Bw0;
+    const int64_t Bw1 = readlane64(off1, 0), nb1 = readlane64(off1 + L1, last) - Bw1;
+    // byte offsets in the wave's range (32-bit whenever the range is below 2^30)
+    const int32_t xo0 = live ? (int32_t)(off0 - Bw0) : (int32_t)min(nb0, (int64_t)INT32_MAX);
+    const int32_t xo1 = live ? (int32_t)(off1 - Bw1) : (int32_t)min(nb1, (int64_t)INT32_MAX);
     // stage [Bw + c0, Bw + c0 + kFStage) of a side in the wave's LDS (16-byte
     // loads from the aligned-down start).  The first stage of BOTH sides is
     // loaded before any tally: a load issued after a global atomic waits for
@@ -2863,16 +2874,17 @@ __global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
 #pragma unroll 1
     for (int side = 0; side < 2; ++side) {
       const uint8_t* src = side ? a.down : a.up;
-      // (selects, not off[side]: a runtime index would put the arrays in scratch)
-      const int64_t fo = side ? off[1] : off[0], fe = side ? end[1] : end[0], frs = side ? rs[1] : rs[0];
+      // (selects, not arrays indexed by side: a runtime index would put them in scratch)
+      const int32_t L = side ? L1 : L0, frs = side ? rw1 : rw0, xo = side ? xo1 : xo0;
       const int64_t Bw = side ? Bw1 : Bw0, nb = side ? nb1 : nb0;
       if (nb <= 0) continue;
-      const int64_t L = fe - fo;
       const int32_t w032 = s_w0[side] >= 0 ? (int32_t)s_w0[side] : -(1 << 30);  // no window: never a hit
       uint32_t* wn = win[side];
       uint8_t* st = stg[w][side];
-      if (nb >= (1 << 30)) {  // (huge flanks: every lane walks its own; rows < 2^31)
-        for (int64_t j = 0; live && frs >= 0 && j < L; ++j) {
+      if (nb >= (1 << 30)) {  // (huge flanks: every lane walks its own from HBM; rows < 2^31)
+        const int64_t fo = live ? (side ? a.down_off[r] : a.up_off[r]) : 0;
+        const int64_t fl = live ? (side ? a.down_off[r + 1] : a.up_off[r + 1]) - fo : 0;
+        for (int64_t j = 0; frs >= 0 && j < fl; ++j) {
           const int code = code_exact(src[fo + j]);
           if (code < 0) { lerr |= DE_KEY; lread = r < lread ? r : lread; continue; }
           const int32_t row = (int32_t)(frs + j);
@@ -2884,8 +2896,7 @@ __global__ __launch_bounds__(NW * 64) void K_flank(FlankArgs a) {
       }
       // wave-relative byte x of lane l's flank: row = x + rowoff (rs + L <= tot < 2^31;
       // no row: rowoff = INT32_MIN, so every row of the flank is negative)
-      const int xo = live ? (int)(fo - Bw) : (int)nb;
-      const int32_t rowoff = (live && frs >= 0) ? (int32_t)(frs - xo) : INT32_MIN;
+      const int32_t rowoff = (live && frs >= 0) ? frs - xo : INT32_MIN;
       const bool ne = live && L > 0;
       const int nb32 = (int)nb;
       int carry = 0;  // owner (1 + lane) of the previous byte group's last byte

@@ -2747,7 +2747,7 @@ __device__ __forceinline__ int32_t flank_gap(const FlankArgs& a, int64_t r, int 
 }
 
 template <int NW, bool MULTI>  // waves per block; blocks take several chunks (grid capped)
-__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MULTI ? 4 : 6))) void K_flank(FlankArgs a) {
+__global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MULTI || NW < kFW ? 4 : 6))) void K_flank(FlankArgs a) {
   // row r, code c at word 5 r + c: consecutive rows (the bytes of one flank,
   // on consecutive lanes) fall on distinct banks
   __shared__ uint32_t win[2][kWinRows * 5];

@@ -151,6 +151,23 @@ def test_synthetic_full_pileup(pkg, spec):
             _cmp(r, _oracle(smp, mdf, gtf), (spec["seed"], s, mdf, gtf))
 
 
+def test_flank_chunk_ranges_across_samples(pkg):
+    """K_flank with more read chunks than blocks (each block a contiguous range
+    of chunks, its LDS windows re-placed where the range crosses into another
+    sample's hot gaps), long flanks around the per-wave stage, four samples."""
+    specs = [dict(n=600, n_reads=70_000, profile="indel", seed=81, frac_partial=0.3, flank=(0, 64)),
+             dict(n=450, n_reads=70_000, profile="default", seed=82, frac_partial=0.3, flank=(0, 40))]
+    samples = []
+    for sp in specs:
+        syn = pkg.synth.Synth(**sp)
+        samples += [syn.sample(0), syn.sample(1)]
+    n_reads = sum(len(smp["tstart"]) for smp in samples)
+    assert (n_reads + 511) // 512 > 512  # more 512-read chunks than K_flank's 512 blocks
+    res = pkg.engine.pileup(samples, -1.0, 1.0)
+    for s, (smp, r) in enumerate(zip(samples, res)):
+        _cmp(r, _oracle(smp, -1.0, 1.0), ("flank_ranges", s))
+
+
 def test_repeat_launches_identical(pkg):
     """Integer atomics: the result does not depend on wave scheduling."""
     syn = pkg.synth.Synth(n=1200, n_reads=4000, profile="indel", seed=77, frac_partial=0.3)

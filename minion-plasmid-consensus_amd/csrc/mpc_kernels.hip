@@ -2697,11 +2697,11 @@ __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
 // barrier: the lane of a flank starting in the segment marks its start byte
 // in the wave's LDS row, and a max-scan over the segment (a byte's owner is
 // the last flank starting at or before it) gives every byte its flank's lane,
-// whose row offset one ds_bpermute fetches.  Rows of the hot gaps (the
-// block's first reads' gaps: for full-length reads gap 0 upstream, gap n
-// downstream) are tallied in LDS windows, everything else with global
-// atomics.  The only block barriers: window placement (after the first
-// records are loaded) and the flush.
+// whose row offset one ds_bpermute fetches.  Rows of the hot gaps (voted per
+// chunk of reads: for full-length reads gap 0 upstream, gap n downstream) are
+// tallied in LDS windows, everything else with global atomics.  Block
+// barriers: one per chunk (after its records load), and the flush (at the
+// end, or when a block's chunk range crosses into another sample's gaps).
 // ---------------------------------------------------------------------------
 #ifndef MPC_FLANK_WAVES
 #define MPC_FLANK_WAVES 8

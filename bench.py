@@ -82,6 +82,9 @@ C5_PER_GPU = 12
 # profiles/r03_experiments/parse_cus_inflight.txt)
 INFLIGHT = {"c1": 4, "c2": 3, "c3": 2, "c4": 2, "c5": 2}
 PARSE_CUS_INFLIGHT = {"c1": 96, "c2": 192, "c3": 224, "c4": 224, "c5": 192}
+# pipelines in flight per rank at world size > 1 (2 compute + 2 communicator
+# streams = the 4 hardware queues a process gets)
+MAX_PIPELINES_DIST = 2
 PORT_SAMPLE_BASES = 2_500_000_000  # bound of the live CPU-port timing (~6 s of C at ~4e8 b/s)
 E2E_CONFIGS = ("c1", "c2", "c3", "c4", "c5")
 
@@ -245,6 +248,26 @@ def kernel_roofline(pkg, eng, cfg, reps, torch):
     return out
 
 
+def traffic_record(cfg, world):
+    """(HBM bytes per K_parse launch, record file) from rocprofv3 PMC passes for
+    this config at this GPU count: profiles/pmc_traffic_<cfg>.json (N = 1) or
+    pmc_traffic_<cfg>_w<N>.json (one rank's shard of the N-shard plan measured on
+    one GPU, scripts/shard_traffic.sh).  C5 runs replicas (every GPU the N = 1
+    plan over its own plasmids): its N = 1 record.  (None, None) if absent."""
+    names = [f"pmc_traffic_{cfg}.json"] if world == 1 else [f"pmc_traffic_{cfg}_w{world}.json"]
+    if world > 1 and cfg == "c5":
+        names.append(f"pmc_traffic_{cfg}.json")
+    for nm in names:
+        try:
+            tr = json.load(open(os.path.join(REPO, "profiles", nm)))
+        except (OSError, ValueError):
+            continue
+        n_ok = tr.get("n_gpus", 1) == world or (cfg == "c5" and tr.get("n_gpus", 1) == 1)
+        if tr.get("config") == cfg and tr.get("kernel") == "K_parse" and n_ok:
+            return tr.get("hbm_bytes_per_launch"), "profiles/" + nm
+    return None, None
+
+
 def launch_ranks(n, argv):
     """``bench.py --gpus N`` (N > 1) started WITHOUT a launcher: run the same
     command as N rank processes (one per GPU) under torch.distributed.run, as a
@@ -293,9 +316,9 @@ def main():
                     help="CUs the parse grid is sized for with batches in flight (default: per config)")
     ap.add_argument("--dist", action="store_true",
                     help="take the distributed path (process group + dist.DistExchange) even at WORLD_SIZE=1")
-    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto",
+    ap.add_argument("--graph", choices=("auto", "on", "off"), default="auto", nargs="?", const="on",
                     help="distributed path: replay every pipeline's step from a HIP graph (no host dispatch); "
-                         "auto = on for RCCL at world size > 1")
+                         "auto = on for RCCL at world size > 1; a bare --graph = on")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-e2e", action="store_true")
     ap.add_argument("--hbm-config", default="c3", type=lambda s: s.strip().lower(),
@@ -344,6 +367,12 @@ def main():
     # batches, as a sequencing run produces; every step is still one full pass
     # over one batch)
     R = max(1, args.inflight if args.inflight is not None else INFLIGHT[cfg])
+    if world > 1 and args.inflight is None and cfg != "c5":
+        # a rank's pipelines each drive a compute stream AND an RCCL communicator
+        # stream; a process gets GPU_MAX_HW_QUEUES = 4 hardware queues, and streams
+        # beyond that share queues in order (a shared queue can stall one
+        # pipeline's collective behind another's compute, on every rank): 2 + 2
+        R = min(R, MAX_PIPELINES_DIST)
     # with batches in flight the parse grid is sized for fewer CUs, so the other
     # batch's post-parse kernels (which cannot share a CU with the parse: it holds
     # every VGPR) run beside it; measured per config at its default R
@@ -369,6 +398,11 @@ def main():
     def step(k):
         with torch.cuda.stream(streams[k % R]):
             runners[k % R].step(mdf, gtf)
+    eager_step = step
+
+    def calls_of(r):
+        """(max depth, device call rows) of every sample: a step's full result."""
+        return [(int(x["max_depth"]), x["raw"].tobytes()) for x in r.fetch()]
 
     batch = runner.batch
     aligned = batch.aligned_bases
@@ -401,6 +435,8 @@ def main():
         graph_note, want_graph = "graph replay needs RCCL (host-staged gloo exchanges): eager steps", False
     if want_graph and use_dist and cfg != "c5":
         graphs, ok = [], 1
+        # the eager step's calls (same mdf / gtf): the replayed step must give them
+        eager_calls = [calls_of(r) for r in runners]
         try:
             for r in runners:
                 g = torch.cuda.CUDAGraph()
@@ -425,7 +461,16 @@ def main():
             torch.cuda.synchronize()
             for r in runners:
                 r.check()
-            graph_note = "steps replayed from HIP graphs (one per pipeline)"
+            # the replayed step's calls equal the eager step's on
+            # every pipeline of every rank, else every rank steps eagerly
+            same = all(calls_of(r) == c for r, c in zip(runners, eager_calls))
+            t = torch.tensor([1 if same else 0], dtype=torch.int64, device=coll_dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MIN)
+            if int(t.item()) == 1:
+                graph_note = "steps replayed from HIP graphs (one per pipeline), calls checked against the eager step"
+            else:
+                step = eager_step
+                graph_note = "a replayed step's calls differed from the eager step's (some rank): eager steps"
         elif graph_note is None:
             graph_note = "another rank failed to capture: eager steps"
 
@@ -511,13 +556,7 @@ def main():
     geo = plan.info()
     alg_bytes = batch.cs_bytes + 24 * batch.n_reads
     achieved = alg_bytes / (k_ms * 1e-3) / 1e9
-    traffic = None
-    try:
-        tr = json.load(open(os.path.join(REPO, "profiles", f"pmc_traffic_{cfg}.json")))
-        if tr.get("config") == cfg and tr.get("kernel") == "K_parse" and tr.get("n_gpus", 1) == world:
-            traffic = tr.get("hbm_bytes_per_launch")
-    except (OSError, ValueError):
-        pass
+    traffic, traffic_src = traffic_record(cfg, world)
 
     cpu = e2e = hbm = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
@@ -562,6 +601,7 @@ def main():
                      if R > 1 else "value = aligned bases of K steps / wall time, one batch at a time"),
             "roofline": {"bound": ROOF_BOUND, "kernel": "K_parse", "achieved": achieved, "peak": HBM_PEAK_GBS,
                          "unit": "GB/s", "frac": achieved / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_record": traffic_src,
                          "alg_bytes_per_launch": alg_bytes, "mean_launch_us": k_ms * 1e3,
                          "plan": "parse grid on all 256 CUs, nothing beside it (a single batch's launch)",
                          "limiter": LIMITER, "input_l3_resident": batch_l3_resident(cfg)},

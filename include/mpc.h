@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MPC_ABI_VERSION 7
+#define MPC_ABI_VERSION 8
 
 /* return codes */
 #define MPC_OK 0
@@ -56,17 +56,21 @@ extern "C" {
 #define MPC_DE_KEY 8u      /* written base not in ACGT (KeyError, :61 / :71) */
 #define MPC_DE_CAPACITY 16u /* row capacity too small: re-plan with status[MPC_ST_ROWS_NEEDED] */
 #define MPC_DE_INTERNAL 32u /* invariant violated (bug) */
-#define MPC_DE_UNSUPPORTED 64u /* input the reference accepts but this engine does not: a negative target
-                                  start whose upstream flank, '+' insertion or downstream flank Python's
-                                  negative index wrap would write into an ODD (reference-base) position
-                                  (tests/golden/n_neg_ins, n_neg_flank, n_neg_end); a ':' / '-' advance of
-                                  2^22 or more from a negative coordinate; tstart < MPC_TSTART_MIN */
+#define MPC_DE_UNSUPPORTED 64u /* input the reference accepts but this engine does not: a ':' / '-' advance
+                                  of 2^22 or more from a negative coordinate; tstart < MPC_TSTART_MIN; a
+                                  write into a wrapped ODD position (below) in a plan that declared no
+                                  negative starts (mpc_input.neg_reads = 0) or with n_shards > 1 */
 
 /* Lowest target start the engine takes.  Negative starts (minimap2 never
  * writes one) follow the reference's Python negative indexing (:222,
  * :300-303): matches and deletions below 0 write nothing, a '*' below 0 writes
  * a one-base LEFT string at gap n + 1 + i, an index below -(2n+1) raises
- * IndexError; a write into a wrapped odd position is MPC_DE_UNSUPPORTED. */
+ * IndexError.  An upstream flank or '+' insertion at a coordinate i in [-n, 0)
+ * (:303, :81-87 -> obsarr[2i] = odd position n + i) and the downstream flank of
+ * a read ending there (:323) add slots to a reference-base position: its
+ * slot list is replayed like a gap's (:37-72) over those strings and the
+ * one-base writes of the reads covering it, in read order (single shard;
+ * the plan sizes the event list from mpc_input.neg_reads / neg_cs_bytes). */
 #ifndef MPC_TSTART_MIN
 #define MPC_TSTART_MIN (-(1 << 28))
 #endif
@@ -79,6 +83,8 @@ extern "C" {
 #define MPC_ST_UNITS 4       /* internal: work units of the bucketed event tallies */
 #define MPC_ST_RSORT_PATH 5  /* internal: sort of the mixed RIGHT events -- 0 one workgroup (planned), 1 the
                                multi-workgroup path ran, 2 it was planned but fell back to one workgroup */
+#define MPC_ST_WRAP_EVENTS 6 /* strings written into wrapped odd positions (negative starts, see above) */
+#define MPC_ST_WRAP_POS 7    /* internal: odd positions that received them */
 #define MPC_ST_WORDS 8
 
 /* Per-read inputs, already in HBM.  One sample = one (assembly, PAF) pair, e.g.
@@ -126,6 +132,12 @@ typedef struct {
    * batches' post-parse kernels run beside it (they cannot share a CU with the
    * parse, which holds every VGPR of the CUs it runs on). */
   int32_t parse_cus;
+  /* reads with tstart < 0 and their cs bytes (host counts; 0, 0 when there
+   * are none).  They bound the strings Python's negative wrap writes into odd
+   * positions (upstream / downstream flanks, '+' insertions at i in [-n, 0));
+   * a plan sized with 0 reports such a write as MPC_DE_UNSUPPORTED. */
+  int64_t neg_reads;
+  int64_t neg_cs_bytes;
 } mpc_input;
 
 typedef struct mpc_plan mpc_plan;
@@ -202,7 +214,7 @@ int mpc_plan_get_info(const mpc_plan* plan, mpc_plan_info* info);
  * struct against it, tests/test_abi.py): returns sizeof(mpc_input) and, when
  * offsets != NULL, writes the byte offset of the first min(cap, field count)
  * fields in declaration order into offsets[].  Field count: MPC_INPUT_FIELDS. */
-#define MPC_INPUT_FIELDS 22
+#define MPC_INPUT_FIELDS 24
 size_t mpc_input_layout(size_t* offsets, int cap);
 /* update the per-read device pointers (same shape) without re-planning */
 int mpc_plan_set_input(mpc_plan* plan, const mpc_input* in);

@@ -169,6 +169,33 @@ struct Ovf {  // long insertion (len > kInsInline), tallied by K_flank
   int32_t pad[3];
 };
 
+// A string Python's negative index wrap writes into an ODD position: with i in
+// [-n, 0), obsarr[2 i] is obsarr[2 (n + i) + 1], the reference base n + i.  An
+// upstream flank at tstart = i (:303) or a '+' at i (:81-87) is a LEFT string
+// there, the downstream flank of a read ending at i (:323) a RIGHT string.
+// K_parse lists them (rare: minimap2 never writes a negative start); the
+// position's slot list is then replayed like a gap's (K_woprep, K_wocover,
+// K_layout<true>, K_worows).
+enum { kWoUp = 0, kWoIns = 1, kWoDown = 2 };  // (order within one read: upstream, cs, downstream)
+struct WoEv {
+  int32_t g;     // global index of the odd position: gbase[s] + (n + i)
+  int32_t read;  // local read
+  int32_t len;   // '+': operand bytes (flanks: from the read's offsets)
+  int32_t type;  // kWo*
+  int64_t src;   // '+': absolute cs offset of the operand
+};
+struct WoPos {   // one odd position holding such strings
+  int32_t g, beg, end;  // its events [beg, end) in the sorted list
+  int32_t run0, nrun;   // its runs (LEFT events between consecutive RIGHT ones)
+  int32_t lo, F, row0;  // replayed lo, slots, first row (K_layout<true>)
+};
+struct WoRun {
+  int32_t M, R;         // longest LEFT string of the run / RIGHT string closing it
+  int32_t hiR, loR;     // replayed hi seen by its LEFT events / lo seen by its RIGHT event
+  uint32_t C[4];        // one-base LEFT writes of the reads covering the position (:79, :96)
+};
+constexpr int64_t kWoCapMax = 1 << 22;  // event list bound (the single-workgroup sort)
+
 // Insertion events (what K_left reads): 4 bytes, bases (8 bits, 2 per base in
 // string order) | (len-1) << 8 | gap within its kBW-gap bucket << 10 | read
 // relative to the parse workgroup's first read << 16 (< 2^15: wg_reads_cap);
@@ -230,6 +257,9 @@ struct Dev {  // device-side views of the plan for the small kernels (passed by 
   uint32_t* runt;                    // [Ng+G][4][4] per run: inline insertion bases by slot from the right end
   uint32_t* res; int32_t* keep; int32_t* ksum; uint32_t* calls; int32_t* ncalls; uint32_t* maxdepth;
   int32_t* srow;                     // [S] first row of every sample (K_layout)
+  // strings in wrapped odd positions (negative starts; wo_cap 0: none planned)
+  WoEv* wo; uint64_t* wo_key; uint32_t* wo_idx; int32_t* wo_erun; WoPos* wo_pos; WoRun* wo_run;
+  int64_t wo_cap, wo_p2;             // list capacity, its power-of-two sort size
   double mdf, gtf;
 };
 
@@ -387,6 +417,7 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
   // tally mode 3: substitutions as 2-byte events per (wave, position window),
   // tallied by K_subs (0 windows: global atomics)
   uint16_t* subev; uint32_t* subev_cnt; int64_t subev_cap; int32_t sub_wins;
+  WoEv* wo; int64_t wo_cap;  // strings written into wrapped odd positions (negative starts only)
 };
 
 // Substitution events (tally mode 3, references too long for LDS substitution
@@ -485,6 +516,19 @@ __device__ __forceinline__ void push_ovf(const ParseArgs& a, int64_t off, int64_
   } else {
     atomicOr(&a.status[MPC_ST_FLAGS], DE_INTERNAL);
   }
+}
+
+// a string into a wrapped odd position (WoEv); returns the data error to flag:
+// none, or DE_UNSUP when the plan has no room (declared no negative starts,
+// several shards)
+__device__ __forceinline__ uint32_t push_wo(const ParseArgs& a, int g, int64_t r, int type, int len, int64_t src) {
+  if (a.wo_cap <= 0) return DE_UNSUP;
+  const uint32_t slot = atomicAdd(&a.status[MPC_ST_WRAP_EVENTS], 1u);
+  if ((int64_t)slot >= a.wo_cap) return DE_UNSUP;
+  WoEv e;
+  e.g = g; e.read = (int32_t)r; e.len = len; e.type = type; e.src = src;
+  a.wo[slot] = e;
+  return 0u;
 }
 
 __device__ __forceinline__ void flag_read(const ParseArgs& a, uint32_t err, int64_t r) {
@@ -807,7 +851,12 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, uint3
 // 1-3), insertion events placed once into 64-event pages of their (workgroup,
 // bucket) (parse_place_event), LEFT-gap bits (LDS bitmap).  Epilogue: flush
 // the tallies, list every bucket's pages (parse_epilogue).
-template <int TM, int WIN>
+// NK: the plan holds reads with a negative tstart (mpc_input.neg_reads): the
+// kernel carries the rounds of Python's negative index wrap (NEG below),
+// taken by the workgroups that hold such a read; without NK nothing of it is
+// compiled in (its registers would bound every plan's kernel), and a negative
+// tstart is MPC_DE_UNSUPPORTED (parsed from 0, never an out-of-range write).
+template <int TM, int WIN, bool NK>
 __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   constexpr int CH = WIN / 64;
   static_assert(WIN <= kMaxWin, "coordinate bound (kMaxWin)");
@@ -868,12 +917,17 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   // none of it)
   // (an OR through cnext[2], not __syncthreads_or: that one takes static LDS
   // the planner's budget does not hold)
-  bool has_neg = false;
-  for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) has_neg |= a.tstart[r] < 0;
-  __syncthreads();
-  if (ballot(has_neg) && lane() == 0) atomicOr(cnext + 2, 1u);
-  __syncthreads();
-  const bool wg_neg = uniform_i32((int)cnext[2]) != 0;
+  bool wg_neg = false;
+  if constexpr (NK) {
+    bool has_neg = false;
+    for (int64_t r = r0 + threadIdx.x; r < r1; r += blockDim.x) has_neg |= a.tstart[r] < 0;
+    __syncthreads();
+    if (ballot(has_neg) && lane() == 0) atomicOr(cnext + 2, 1u);
+    __syncthreads();
+    wg_neg = uniform_i32((int)cnext[2]) != 0;
+  } else {
+    __syncthreads();  // the chunk table, counters and cleared tallies above are in place
+  }
 
   auto odd_sub = [&](int pos, int code) {
     if (lds_sub) atomicAdd(sub_l + 2 * pos + (code >> 1), 1u << (16 * (code & 1)));
@@ -1022,11 +1076,18 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     if (inwin) {
       const int q = l + 1;
       const bool up = uo_nx != cur.uo, dn = dno_nx != cur.dno;  // flank lengths < 2^32
-      const int ts = cur.ts;
       uint32_t derr = 0;
+      // (a kernel without the negative rounds parses a negative start from 0, flagged)
+      const int ts = !NEG && cur.ts < 0 ? 0 : cur.ts;
+      if (!NEG && cur.ts < 0) derr |= DE_UNSUP;
       // obsarr[2 tstart] (:303) with Python's negative wrap: below -n past the
-      // front (IndexError), in [-n, 0) a wrapped ODD position (not supported)
-      if (up && ts < 0) derr |= ts + n >= 0 ? DE_UNSUP : DE_INDEX;
+      // front (IndexError), in [-n, 0) a LEFT string at the wrapped ODD
+      // position n + tstart (listed; only NEG chunks see a negative tstart)
+      if (up && ts < 0) {
+        if (ts + n < 0) derr |= DE_INDEX;
+        else if constexpr (NEG) derr |= push_wo(a, gb + ts + n, rs0 + l, kWoUp, 0, 0);
+        else derr |= DE_INTERNAL;
+      }
       if (ts < MPC_TSTART_MIN) derr |= DE_UNSUP;
       if (up && ts > n) derr |= DE_INDEX;             // leftIndel(2*i) past the end
       if (o_nx <= cur.o) derr |= DE_OP;               // processOperation('', '')
@@ -1299,18 +1360,18 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       // refarr / obsarr take index x at len + x for x in [-(2n+1), 0)
       // (Python list indexing).  A ':' or '-' there writes nothing
       // (the wrapped refarr index is even: ''); a '*' at i < 0 writes its base
-      // as a one-base LEFT string at gap n + 1 + i; a '+' at i in [-n, 0) would
-      // write slots into a wrapped ODD position: unsupported (MPC_DE_UNSUPPORTED)
-      bool wrap = false, unsup = false;
+      // as a one-base LEFT string at gap n + 1 + i; a '+' at i in [-n, 0) is a
+      // LEFT string at the wrapped ODD position n + i (listed, push_wo)
+      bool wrap = false, unsup = false, wo_ins = false;
       int di = i, gi = i, li = olen_e;  // deletion start, LEFT gap and length
       if constexpr (NEG) {
         const bool mat = (kind == 1) | (kind == 2);
         bad_i = ((adv0 > 0) & (((iu + n + 1) | (n - i)) < 0)) | (mat & (((i + n + 1) | (n - adv - i)) < 0)) |
                 ((kind == 3) & (((i + n) | (n - i)) < 0));
-        // '+' into a wrapped odd position; or an advance clamped at kAdvCap
-        // from a negative coordinate (its true end may still be <= n)
-        unsup = ((kind == 3) & (i < 0) & (i + n >= 0)) | ((adv0 >= kAdvCap) & (iu < 0)) |
-                ((adv >= kAdvCap) & (i < 0) & ((kind == 1) | (kind == 4)));
+        // an advance clamped at kAdvCap from a negative coordinate (its true
+        // end may still be <= n)
+        unsup = ((adv0 >= kAdvCap) & (iu < 0)) | ((adv >= kAdvCap) & (i < 0) & ((kind == 1) | (kind == 4)));
+        wo_ins = (kind == 3) & (i < 0) & (i + n >= 0);
         wrap = (kind == 2) & (i < 0);
         di = i < 0 ? 0 : i;
         gi = wrap ? i + n + 1 : i;
@@ -1318,7 +1379,8 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       }
       uint32_t te = err | (bad_i ? DE_INDEX : 0u) | (unsup ? DE_UNSUP : 0u);
       const int rl = q_read;
-      const bool ok = te == 0;
+      if (NEG && wo_ins && te == 0) te |= push_wo(a, gb + i + n, rl, kWoIns, olen_e, A + sx + 1);
+      const bool ok = te == 0 && !wo_ins;
       if (ok & (kind == 2) & !wrap & (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
       const bool del = NEG ? ok & (kind == 4) & (di < n) & (i + olen_e > di) : ok & (kind == 4) & (i >= 0) & (i < n);
       if (del) {
@@ -1349,9 +1411,14 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
         const int dnf = q_iend & (1 << 30);
         if (dnf && ia > n) te |= DE_INDEX;   // rightIndel(2*i) past the end
-        // ... or, wrapped, past the front / into an odd position (unsupported)
-        if (NEG && dnf && ia < 0) te |= ia + n >= 0 ? DE_UNSUP : DE_INDEX;
-        W.s_iend[q] = ie | dnf;
+        // ... or, wrapped, past the front, or a RIGHT string at the odd
+        // position n + ia (listed; i_end n + 1: no gap row for it)
+        int iw = ie;
+        if (NEG && dnf && ia < 0) {
+          if (ia + n < 0) te |= DE_INDEX;
+          else { te |= push_wo(a, gb + ia + n, rl, kWoDown, 0, 0); iw = n + 1; }
+        }
+        W.s_iend[q] = iw | dnf;
         const int ts = NEG && q_ts < 0 ? 0 : q_ts;  // matches below 0 write nothing
         const int e2 = ie > n ? n : ie;
         if (ts < e2) { depth_inc(ts); depth_dec(e2); }
@@ -1394,8 +1461,12 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   if (TM == 3 && l < a.sub_wins) a.subev_cnt[((int64_t)blockIdx.x * kMaxCh + chk) * kMaxSubWins + l] = nsub_v;
   }  // chunks
   };
-  if (wg_neg) chunks(std::true_type{});
-  else chunks(std::false_type{});
+  if constexpr (NK) {
+    if (wg_neg) chunks(std::true_type{});
+    else chunks(std::false_type{});
+  } else {
+    chunks(std::false_type{});
+  }
   MPC_SEG(5);
   // every LDS-DMA was waited for by the window after it (one is issued only
   // when another window follows); drain anyway before the LDS is reused
@@ -2490,6 +2561,217 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
 }
 
 // ---------------------------------------------------------------------------
+// Wrapped odd positions (negative target starts; WoEv).  An odd position that
+// receives LEFT strings (upstream flanks :303, '+' insertions :81-87) or
+// RIGHT strings (downstream flanks :323) through Python's negative index wrap
+// grows a slot list like a gap's (:37-72), and its one-base writes -- the
+// match or substitution of every read covering the reference base (:79, :96)
+// -- are LEFT strings of length 1 in the same replay.  Its runs are split at
+// its RIGHT strings in read order (a read's own LEFT strings there precede its
+// RIGHT one; a read ending at n + i < 0 never reaches the base itself).
+//   K_woprep       one workgroup: sorts the list by (position, read, kind);
+//                  the positions, their runs, each string's run, the longest
+//                  LEFT / the closing RIGHT string per run
+//   K_wocover      one thread per read: walks its cs (:306-320) and counts its
+//                  one-base write at every listed position it covers into the
+//                  run it falls in
+//   K_layout<true> replays each listed position's runs (F slots, F rows)
+//   K_worows       the strings and the one-base counts onto those rows
+// None of it runs in plans without negative starts (mpc_input.neg_reads).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint64_t wo_sort_key(const WoEv& e) {
+  return ((uint64_t)(uint32_t)e.g << 32) | ((uint64_t)(uint32_t)e.read << 2) | (uint64_t)(uint32_t)e.type;
+}
+__device__ __forceinline__ int64_t wo_key_read(uint64_t k) { return (int64_t)((k >> 2) & 0x3fffffffu); }
+
+// exclusive scan of x[0, n) in place by one workgroup; returns the total
+__device__ int64_t block_scan_excl(int32_t* x, int64_t n, int32_t* s_w) {
+  int64_t carry = 0;
+  const int w = threadIdx.x >> 6, l = lane(), nw = (int)(blockDim.x >> 6);
+  for (int64_t b0 = 0; b0 < n; b0 += blockDim.x) {
+    const int64_t k = b0 + threadIdx.x;
+    const int v = k < n ? x[k] : 0;
+    const int inc = wave_scan_i32(v);
+    if (l == 63) s_w[w] = inc;
+    __syncthreads();
+    int pre = 0, tot = 0;
+    for (int j = 0; j < nw; ++j) { pre += j < w ? s_w[j] : 0; tot += s_w[j]; }
+    if (k < n) x[k] = (int32_t)(carry + pre + inc - v);
+    carry += tot;
+    __syncthreads();
+  }
+  return carry;
+}
+
+// first listed position with g >= x among [0, np)
+__device__ __forceinline__ int wo_lower(const WoPos* pos, int np, int64_t x) {
+  int lo = 0, hi = np;
+  while (lo < hi) {
+    const int mid = (lo + hi) >> 1;
+    if (pos[mid].g < x) lo = mid + 1; else hi = mid;
+  }
+  return lo;
+}
+
+__device__ __forceinline__ int32_t wo_len(const Dev& d, const WoEv& e) {
+  if (e.type == kWoIns) return e.len;
+  const int64_t* off = e.type == kWoUp ? d.up_off : d.down_off;
+  const int64_t L = off[e.read + 1] - off[e.read];
+  return L > 0x7fffffff ? 0x7fffffff : (int32_t)L;
+}
+
+__global__ __launch_bounds__(1024) void K_woprep(Dev d) {
+  __shared__ int32_t s_w[16];
+  const int64_t n = min<int64_t>((int64_t)d.status[MPC_ST_WRAP_EVENTS], d.wo_cap);
+  if (n == 0) {
+    if (threadIdx.x == 0) d.status[MPC_ST_WRAP_POS] = 0u;
+    return;
+  }
+  int64_t P2 = 1;
+  while (P2 < n) P2 <<= 1;
+  uint64_t* key = d.wo_key;
+  uint32_t* idx = d.wo_idx;
+  for (int64_t k = threadIdx.x; k < P2; k += blockDim.x) {
+    key[k] = k < n ? wo_sort_key(d.wo[k]) : ~0ull;
+    idx[k] = (uint32_t)k;
+  }
+  __syncthreads();
+  // bitonic sort of (key, idx): keys are distinct but for a read's '+' strings
+  // at one position, which are LEFT strings of one run (any order)
+  for (int64_t size = 2; size <= P2; size <<= 1)
+    for (int64_t stride = size >> 1; stride > 0; stride >>= 1) {
+      for (int64_t t = threadIdx.x; t < P2 / 2; t += blockDim.x) {
+        const int64_t lo = 2 * stride * (t / stride) + (t % stride), hi = lo + stride;
+        const bool asc = (lo & size) == 0;
+        const uint64_t a = key[lo], b = key[hi];
+        if ((a > b) == asc && a != b) {
+          key[lo] = b; key[hi] = a;
+          const uint32_t x = idx[lo]; idx[lo] = idx[hi]; idx[hi] = x;
+        }
+      }
+      __syncthreads();
+    }
+  // positions: segments of equal g
+  int32_t* tmp = d.wo_erun + d.wo_cap;
+  auto starts = [&](int64_t k) { return k == 0 || (key[k] >> 32) != (key[k - 1] >> 32); };
+  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) tmp[k] = starts(k) ? 1 : 0;
+  __syncthreads();
+  const int64_t npos = block_scan_excl(tmp, n, s_w);  // tmp[k] = positions starting before k
+  for (int64_t k = threadIdx.x; k < n; k += blockDim.x) {
+    const bool st = starts(k);
+    const int32_t p = st ? tmp[k] : tmp[k] - 1;
+    if (st) { d.wo_pos[p].g = (int32_t)(key[k] >> 32); d.wo_pos[p].beg = (int32_t)k; }
+    if (k == n - 1 || starts(k + 1)) d.wo_pos[p].end = (int32_t)(k + 1);
+  }
+  __syncthreads();
+  // runs per position: one more than its RIGHT strings
+  for (int64_t p = threadIdx.x; p < npos; p += blockDim.x) {
+    int32_t m = 0;
+    for (int32_t e = d.wo_pos[p].beg; e < d.wo_pos[p].end; ++e) m += (int32_t)(key[e] & 3u) == kWoDown;
+    d.wo_pos[p].nrun = m + 1;
+    tmp[p] = m + 1;
+  }
+  __syncthreads();
+  block_scan_excl(tmp, npos, s_w);
+  for (int64_t p = threadIdx.x; p < npos; p += blockDim.x) {
+    WoPos& P = d.wo_pos[p];
+    const int32_t run0 = tmp[p];
+    P.run0 = run0;
+    for (int32_t j = 0; j < P.nrun; ++j) {
+      WoRun z;
+      z.M = 0; z.R = 0; z.hiR = 0; z.loR = 0; z.C[0] = z.C[1] = z.C[2] = z.C[3] = 0u;
+      d.wo_run[run0 + j] = z;
+    }
+    int32_t j = 0;
+    for (int32_t e = P.beg; e < P.end; ++e) {
+      d.wo_erun[e] = j;  // RIGHT strings before it: its run (a RIGHT string closes run j)
+      const WoEv ev = d.wo[idx[e]];
+      const int32_t L = wo_len(d, ev);
+      WoRun& R = d.wo_run[run0 + j];
+      if (ev.type == kWoDown) { R.R = L; ++j; }
+      else if (L > R.M) R.M = L;
+    }
+  }
+  if (threadIdx.x == 0) d.status[MPC_ST_WRAP_POS] = (uint32_t)npos;
+}
+
+// one thread per read: the read's one-base writes (:79 matches, :96
+// substitutions) at the listed positions, counted per run
+__device__ void wo_cover_read(const Dev& d, int np, int64_t r);
+__global__ __launch_bounds__(256) void K_wocover(Dev d) {
+  const int np = (int)d.status[MPC_ST_WRAP_POS];
+  if (np == 0) return;
+  for (int64_t r = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; r < d.N; r += (int64_t)gridDim.x * blockDim.x)
+    wo_cover_read(d, np, r);
+}
+__device__ void wo_cover_read(const Dev& d, int np, int64_t r) {
+  const int s = d.sample[r];
+  const int64_t n = d.n_of[s], gb = d.gbase[s];
+  const int pa = wo_lower(d.wo_pos, np, gb), pb = wo_lower(d.wo_pos, np, gb + n);
+  if (pa == pb) return;
+  const uint8_t* ref = d.ref + d.ref_off[s];
+  auto hit = [&](int p, int code) {
+    const WoPos P = d.wo_pos[p];
+    int lo = P.beg, hi = P.end;  // the position's first string from a read >= r
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (wo_key_read(d.wo_key[mid]) < r) lo = mid + 1; else hi = mid;
+    }
+    const int32_t j = lo < P.end ? d.wo_erun[lo] : P.nrun - 1;
+    atomicAdd(&d.wo_run[P.run0 + j].C[code], 1u);
+  };
+  // the tokenizer of :306-320: an operator applies to the operand gathered
+  // after it when the next operator comes with a non-empty operand, the last
+  // one unconditionally.  Data errors were flagged by K_parse: stop there.
+  const int64_t b = d.cs_off[r], e = d.cs_off[r + 1];
+  int64_t i = d.tstart[r], o0 = b, olen = 0;
+  uint32_t op = 0;
+  for (int64_t x = b;; ++x) {
+    const bool end = x >= e;
+    const uint32_t c = end ? 0u : d.cs[x];
+    const bool sp = !end && (c == ':' || c == 'Z' || c == '+' || c == '-' || c == '*');
+    if (!end && !sp) { ++olen; continue; }
+    if (end || olen > 0) {
+      if (op == ':') {
+        int64_t m = 0;
+        if (olen == 0) return;
+        for (int64_t y = o0; y < o0 + olen; ++y) {
+          const uint32_t dc = (uint32_t)d.cs[y] - 0x30u;
+          if (dc > 9u) return;
+          m = m * 10 + dc;
+          if (m > (1ll << 40)) m = 1ll << 40;
+        }
+        const int64_t k0 = i < 0 ? 0 : i, k1 = i + m < n ? i + m : n;
+        for (int p = k0 < k1 ? wo_lower(d.wo_pos, np, gb + k0) : pb; p < pb && d.wo_pos[p].g < gb + k1; ++p) {
+          const int code = base_code_exact(ref[d.wo_pos[p].g - gb]);
+          if (code >= 0) hit(p, code);  // (else KeyError: K_layout flags it)
+        }
+        i += m;
+      } else if (op == '*') {
+        if (olen == 0) return;
+        if (i >= 0 && i < n) {
+          const int p = wo_lower(d.wo_pos, np, gb + i);
+          if (p < pb && d.wo_pos[p].g == gb + i) {
+            const int code = code_upper(d.cs[o0 + olen - 1]);
+            if (code >= 0) hit(p, code);
+          }
+        }
+        i += 1;
+      } else if (op == '-') {
+        i += olen;
+      } else if (op != '+' && op != 'Z') {
+        return;  // unknown operator (:100-102)
+      }
+      if (i >= n) return;  // any later one-base write is past the end
+    }
+    if (end) break;
+    op = c;
+    o0 = x + 1;
+    olen = 0;
+  }
+}
+
+// ---------------------------------------------------------------------------
 // Layout: replay of processBaseString_leftIndel / _rightIndel slot creation.
 // Per gap the list grows at the front (LEFT, right-justified) and at the back
 // (RIGHT, left-justified).  State: lo = slots prepended, hi = slots appended.
@@ -2516,6 +2798,9 @@ constexpr int kGB = MPC_LAYOUT_GAPS;  // gaps per K_layout block (fewer blocks: 
 // running or finished blocks; the spin is bounded (DE_INTERNAL, never a hang).
 // The row capacity is checked per gap (rows that do not fit are not written);
 // the last block sets ROWS_NEEDED and DE_CAP for the re-plan.
+// WO: the plan lists wrapped odd positions (K_woprep); such a position after
+// gap g is replayed here too and takes F rows instead of one.
+template <bool WO>
 __global__ __launch_bounds__(kGB) void K_layout(Dev d, uint32_t epoch) {
   __shared__ int32_t s_w[2][kGB / 64];
   __shared__ int64_t s_pre[2];
@@ -2523,6 +2808,7 @@ __global__ __launch_bounds__(kGB) void K_layout(Dev d, uint32_t epoch) {
   const int64_t nb = (d.G + kGB - 1) / kGB;
   const int64_t g = b * kGB + threadIdx.x;
   int32_t rc = 0, dv = 0;
+  int32_t F = 1, wop = -1;  // rows of the odd position after the gap; its listed index
   int s = 0;
   int64_t p = 0;
   if (g < d.G) {
@@ -2549,7 +2835,32 @@ __global__ __launch_bounds__(kGB) void K_layout(Dev d, uint32_t epoch) {
     }
     s = lo_s;
     p = g - d.gbase[s];
-    rc = lo + hi + (p < d.n_of[s] ? 1 : 0);  // rows of a gap = its slots + the odd position after it
+    if constexpr (WO) {
+      const int np = (int)d.status[MPC_ST_WRAP_POS];
+      const int k = wo_lower(d.wo_pos, np, g);
+      if (p < d.n_of[s] && k < np && d.wo_pos[k].g == g) {
+        // lo / hi of the odd position over its runs; a run's one-base writes
+        // are a LEFT string of length 1
+        const WoPos P = d.wo_pos[k];
+        int32_t wl = 0, wh = 0;
+        for (int32_t j = 0; j < P.nrun; ++j) {
+          WoRun& R = d.wo_run[P.run0 + j];
+          const int32_t c1 = (R.C[0] | R.C[1] | R.C[2] | R.C[3]) != 0u ? 1 : 0;
+          const int32_t m = R.M > c1 ? R.M : c1;
+          R.hiR = wh;
+          if (m - wh > wl) wl = m - wh;
+          if (j + 1 < P.nrun) {
+            R.loR = wl;
+            if (R.R - wl > wh) wh = R.R - wl;
+          }
+        }
+        F = wl + wh;
+        wop = k;
+        d.wo_pos[k].lo = wl;
+        d.wo_pos[k].F = F;
+      }
+    }
+    rc = lo + hi + (p < d.n_of[s] ? F : 0);  // rows of a gap = its slots + the odd position after it
     d.rowcnt[g] = rc;
     dv = d.diff[g];
   }
@@ -2584,7 +2895,7 @@ __global__ __launch_bounds__(kGB) void K_layout(Dev d, uint32_t epoch) {
   if (p == 0) d.srow[s] = (int32_t)rb;  // the consensus kernels' sample table (one load, no gbase chain)
   if (rb + rc > d.row_cap) return;      // does not fit: the last block flags DE_CAP (re-plan)
   const int64_t n = d.n_of[s];
-  const int64_t nslots = (int64_t)rc - (p < n ? 1 : 0);
+  const int64_t nslots = (int64_t)rc - (p < n ? F : 0);
   if (nslots > 0) d.meta[rb] = 2;  // first slot of the gap
   if (p < n) {
     // each shard: its own reads' depth and substitutions (rows are summed over shards)
@@ -2601,8 +2912,9 @@ __global__ __launch_bounds__(kGB) void K_layout(Dev d, uint32_t epoch) {
       else c[rcode] += (uint32_t)match;
     }
     if (fl) atomicOr(&d.status[MPC_ST_FLAGS], fl);
-    reinterpret_cast<uint4*>(d.rows)[rb + nslots] = make_uint4(c[0], c[1], c[2], c[3]);
-    d.meta[rb + nslots] = 3;  // odd row, first (only) slot of its position
+    if (WO && wop >= 0) d.wo_pos[wop].row0 = (int32_t)(rb + nslots);  // rows by K_worows
+    else reinterpret_cast<uint4*>(d.rows)[rb + nslots] = make_uint4(c[0], c[1], c[2], c[3]);
+    d.meta[rb + nslots] = 3;  // odd row, first slot of its position
   }
 }
 
@@ -2957,6 +3269,63 @@ __global__ __launch_bounds__(NW * 64) __attribute__((amdgpu_waves_per_eu(MULTI |
   }
 }
 
+// The rows of the listed wrapped odd positions (K_layout<true> placed them at
+// row0, lo = the replayed slots prepended): a run's one-base writes go to slot
+// lo + hiR - 1; a LEFT string's base bi from its 3' end to lo + hiR - 1 - bi
+// (:55-61), a RIGHT string's base bi to lo - loR + bi (:67-71).  One wave per
+// position (its runs) / per string (its bases on the lanes).
+__global__ __launch_bounds__(256) void K_worows(Dev d) {
+  const int np = (int)d.status[MPC_ST_WRAP_POS];
+  if (np == 0 || (d.status[MPC_ST_FLAGS] & DE_CAP)) return;
+  const int64_t n_ev = min<int64_t>((int64_t)d.status[MPC_ST_WRAP_EVENTS], d.wo_cap);
+  const int l = lane();
+  const int64_t nwaves = (int64_t)gridDim.x * (blockDim.x >> 6);
+  const int64_t gw = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+  for (int64_t p = gw; p < np; p += nwaves) {
+    const WoPos P = d.wo_pos[p];
+    for (int32_t j = l; j < P.nrun; j += 64) {
+      const WoRun R = d.wo_run[P.run0 + j];
+      uint32_t* row = d.rows + ((int64_t)P.row0 + P.lo + R.hiR - 1) * 4;
+#pragma unroll
+      for (int c = 0; c < 4; ++c)
+        if (R.C[c]) atomicAdd(row + c, R.C[c]);
+    }
+  }
+  uint32_t err = 0;
+  int64_t eread = INT64_MAX;
+  for (int64_t e = gw; e < n_ev; e += nwaves) {
+    const WoEv ev = d.wo[d.wo_idx[e]];
+    const WoPos P = d.wo_pos[wo_lower(d.wo_pos, np, ev.g)];
+    const WoRun R = d.wo_run[P.run0 + d.wo_erun[e]];
+    const int64_t L = wo_len(d, ev);
+    const uint8_t* src = ev.type == kWoIns ? d.cs + ev.src
+                       : ev.type == kWoUp  ? d.up + d.up_off[ev.read]
+                                           : d.down + d.down_off[ev.read];
+    for (int64_t bi = l; bi < L; bi += 64) {
+      int code;
+      int64_t slot;
+      if (ev.type == kWoDown) {
+        code = code_exact(src[bi]);
+        slot = (int64_t)P.lo - R.loR + bi;
+      } else {
+        const uint32_t c = src[L - 1 - bi];
+        code = ev.type == kWoIns ? code_upper(c) : code_exact(c);
+        slot = (int64_t)P.lo + R.hiR - 1 - bi;
+      }
+      if (code < 0) {  // KeyError (:61, :71); a '+' base K_parse flagged too
+        err |= DE_KEY;
+        eread = ev.read < eread ? ev.read : eread;
+        continue;
+      }
+      atomicAdd(d.rows + ((int64_t)P.row0 + slot) * 4 + code, 1u);
+    }
+  }
+  if (err) {
+    atomicOr(&d.status[MPC_ST_FLAGS], err);
+    atomicMin(&d.status[MPC_ST_FIRST_READ], (uint32_t)eread);
+  }
+}
+
 // ---------------------------------------------------------------------------
 // Consensus (Steps 5-6, :332-439)
 // ---------------------------------------------------------------------------
@@ -3183,6 +3552,7 @@ struct mpc_plan {
   std::vector<int64_t> ref_len, read_begin;
   std::vector<int32_t> h_n, h_gbase;
   int64_t N = 0, Ng = 0, G = 0, row_cap = 0, runs_cap = 0, ins_cap = 0, ovf_cap = 0, pages_cap = 0;
+  int64_t wo_cap = 0, wo_p2 = 1;  // strings into wrapped odd positions (negative starts): list bound, sort size
   int32_t S = 0;
   int32_t overrides = 0;  // MPC_OVR_* (experiment builds only)
   uint32_t sentinel = 0;
@@ -3207,7 +3577,8 @@ struct mpc_plan {
     // MAXR, M, RUNR adjacent and in this order: one MAX exchange over their span (mpc.h)
     B_DIFF, B_SUB, B_MAXR, B_M, B_RUNR, B_HIR, B_LOR, B_LOF, B_ROWCNT, B_ROWBASE, B_BSUM, B_ROWS,
     B_META, B_RES, B_KEEP, B_KSUM, B_CALLS, B_NCALLS, B_MAXD, B_SROW, B_WPARSE, B_WBC, B_UNITS, B_RUNT,
-    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_SUBSLAB, B_WSUBSUM, B_GCNT, B_KSLOT, B_RSFLAG, B_PGLIST, B_COUNT
+    B_SUBEV, B_SUBCNT, B_WSUB, B_BKCUR, B_WWAVE, B_SUBSLAB, B_WSUBSUM, B_GCNT, B_KSLOT, B_RSFLAG, B_PGLIST,
+    B_WOEV, B_WOKEY, B_WOIDX, B_WOERUN, B_WOPOS, B_WORUN, B_COUNT
   };
   size_t off[B_COUNT];
   size_t sz[B_COUNT];
@@ -3250,6 +3621,9 @@ Dev mpc_plan::dev() const {
   d.res = at<uint32_t>(this, B_RES); d.keep = at<int32_t>(this, B_KEEP); d.ksum = at<int32_t>(this, B_KSUM);
   d.calls = at<uint32_t>(this, B_CALLS); d.ncalls = at<int32_t>(this, B_NCALLS); d.maxdepth = at<uint32_t>(this, B_MAXD);
   d.srow = at<int32_t>(this, B_SROW);
+  d.wo = at<WoEv>(this, B_WOEV); d.wo_key = at<uint64_t>(this, B_WOKEY); d.wo_idx = at<uint32_t>(this, B_WOIDX);
+  d.wo_erun = at<int32_t>(this, B_WOERUN); d.wo_pos = at<WoPos>(this, B_WOPOS); d.wo_run = at<WoRun>(this, B_WORUN);
+  d.wo_cap = wo_cap; d.wo_p2 = wo_p2;
   return d;
 }
 
@@ -3270,17 +3644,24 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.diff = d.diff; a.sub = d.sub;
   a.subev = at<uint16_t>(p, mpc_plan::B_SUBEV); a.subev_cnt = at<uint32_t>(p, mpc_plan::B_SUBCNT);
   a.subev_cap = p->subev_cap; a.sub_wins = p->tally_mode == 3 ? p->sub_wins : 0;
+  a.wo = d.wo; a.wo_cap = d.wo_cap;
   return a;
 }
 
 // instantiated (tally mode, window) pairs; packed modes only with 1 and 2 KiB windows
-static const void* parse_kernel(int tm, int win) {
-  if (tm == 4) return (const void*)K_parse<4, 1024>;
-  if (tm == 2) return win == 1024 ? (const void*)K_parse<2, 1024> : (const void*)K_parse<2, 2048>;
-  if (tm == 3) return win == 1024 ? (const void*)K_parse<3, 1024> : (const void*)K_parse<3, 2048>;
-  if (win == 512) return tm ? (const void*)K_parse<1, 512> : (const void*)K_parse<0, 512>;
-  if (win == 2048) return tm ? (const void*)K_parse<1, 2048> : (const void*)K_parse<0, 2048>;
-  return tm ? (const void*)K_parse<1, 1024> : (const void*)K_parse<0, 1024>;
+template <bool NK>
+static const void* parse_kernel_t(int tm, int win) {
+  if (tm == 4) return (const void*)K_parse<4, 1024, NK>;
+  if (tm == 2) return win == 1024 ? (const void*)K_parse<2, 1024, NK> : (const void*)K_parse<2, 2048, NK>;
+  if (tm == 3) return win == 1024 ? (const void*)K_parse<3, 1024, NK> : (const void*)K_parse<3, 2048, NK>;
+  if (win == 512) return tm ? (const void*)K_parse<1, 512, NK> : (const void*)K_parse<0, 512, NK>;
+  if (win == 2048) return tm ? (const void*)K_parse<1, 2048, NK> : (const void*)K_parse<0, 2048, NK>;
+  return tm ? (const void*)K_parse<1, 1024, NK> : (const void*)K_parse<0, 1024, NK>;
+}
+// the plan's K_parse: with the negative-start rounds only when it holds such reads
+static const void* parse_kernel(const mpc_plan* p) {
+  return p->in.neg_reads > 0 ? parse_kernel_t<true>(p->tally_mode, p->parse_win)
+                             : parse_kernel_t<false>(p->tally_mode, p->parse_win);
 }
 static void launch_subs(const mpc_plan* p, const Dev& d, hipStream_t st) {
   if (p->work_sub.empty()) return;
@@ -3303,20 +3684,9 @@ static void launch_subs(const mpc_plan* p, const Dev& d, hipStream_t st) {
   }
 }
 static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
-  const dim3 g(p->n_parse_wg), b(p->parse_nw * 64);
-  const ParseArgs a = parse_args(p, d);
-  const int tm = p->tally_mode, win = p->parse_win;
-  if (tm == 4) hipLaunchKernelGGL((K_parse<4, 1024>), g, b, p->parse_lds, st, a);
-  else if (tm == 2 && win == 1024) hipLaunchKernelGGL((K_parse<2, 1024>), g, b, p->parse_lds, st, a);
-  else if (tm == 2) hipLaunchKernelGGL((K_parse<2, 2048>), g, b, p->parse_lds, st, a);
-  else if (tm == 3 && win == 1024) hipLaunchKernelGGL((K_parse<3, 1024>), g, b, p->parse_lds, st, a);
-  else if (tm == 3) hipLaunchKernelGGL((K_parse<3, 2048>), g, b, p->parse_lds, st, a);
-  else if (win == 512 && tm) hipLaunchKernelGGL((K_parse<1, 512>), g, b, p->parse_lds, st, a);
-  else if (win == 512) hipLaunchKernelGGL((K_parse<0, 512>), g, b, p->parse_lds, st, a);
-  else if (win == 2048 && tm) hipLaunchKernelGGL((K_parse<1, 2048>), g, b, p->parse_lds, st, a);
-  else if (win == 2048) hipLaunchKernelGGL((K_parse<0, 2048>), g, b, p->parse_lds, st, a);
-  else if (tm) hipLaunchKernelGGL((K_parse<1, 1024>), g, b, p->parse_lds, st, a);
-  else hipLaunchKernelGGL((K_parse<0, 1024>), g, b, p->parse_lds, st, a);
+  ParseArgs a = parse_args(p, d);
+  void* args[] = {&a};
+  (void)hipLaunchKernel(parse_kernel(p), dim3(p->n_parse_wg), dim3(p->parse_nw * 64), args, (size_t)p->parse_lds, st);
 }
 
 static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
@@ -3432,7 +3802,7 @@ size_t mpc_input_layout(size_t* off, int cap) {
                              MPC_F(up_off), MPC_F(down), MPC_F(down_off), MPC_F(sample), MPC_F(n_samples),
                              MPC_F(h_ref_len), MPC_F(h_read_begin), MPC_F(n_reads), MPC_F(cs_bytes), MPC_F(cs_base),
                              MPC_F(read_offset), MPC_F(n_reads_global), MPC_F(shard), MPC_F(n_shards),
-                             MPC_F(h_cs_off), MPC_F(parse_cus)};
+                             MPC_F(h_cs_off), MPC_F(parse_cus), MPC_F(neg_reads), MPC_F(neg_cs_bytes)};
 #undef MPC_F
   static_assert(sizeof(o) / sizeof(o[0]) == MPC_INPUT_FIELDS, "mpc_input field table");
   for (int k = 0; off && k < cap && k < MPC_INPUT_FIELDS; ++k) off[k] = o[k];
@@ -3475,6 +3845,12 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   p->runs_cap = p->Ng + p->G;
   p->ins_cap = in->cs_bytes / 2 + 3 * p->N + 16;  // insertions (>= 2 cs bytes each) + slack per read
   p->ovf_cap = in->cs_bytes / 6 + 16;
+  // strings Python's negative wrap writes into odd positions: <= 2 flanks per
+  // read with a negative start plus its '+' insertions (>= 2 cs bytes each);
+  // one shard only (the replay needs every string of a position)
+  if (in->neg_reads < 0 || in->neg_cs_bytes < 0) { delete p; return fail(MPC_E_ARG, "negative neg_reads / neg_cs_bytes"); }
+  p->wo_cap = p->n_shards == 1 && in->neg_reads > 0 ? std::min<int64_t>(kWoCapMax, 2 * in->neg_reads + in->neg_cs_bytes / 2 + 16) : 0;
+  while (p->wo_p2 < p->wo_cap) p->wo_p2 <<= 1;
   int eb = 1;
   while ((1ll << eb) <= p->G + 1) ++eb;
   p->end_bit = eb;
@@ -3752,6 +4128,12 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
   set(mpc_plan::B_WWAVE, (int64_t)p->work_wave.size(), 4);
   set(mpc_plan::B_SUBSLAB, MPC_SUBS_SLAB ? (int64_t)(p->work_sub.size() / 4) * kSubWin * 2 : 0, 4);
   set(mpc_plan::B_WSUBSUM, (int64_t)p->work_subsum.size(), 4);
+  set(mpc_plan::B_WOEV, p->wo_cap, sizeof(WoEv));
+  set(mpc_plan::B_WOKEY, p->wo_cap ? p->wo_p2 : 0, 8);
+  set(mpc_plan::B_WOIDX, p->wo_cap ? p->wo_p2 : 0, 4);
+  set(mpc_plan::B_WOERUN, 2 * p->wo_cap, 4);  // run of every sorted string, then K_woprep's scratch
+  set(mpc_plan::B_WOPOS, p->wo_cap, sizeof(WoPos));
+  set(mpc_plan::B_WORUN, p->wo_cap ? 2 * p->wo_cap + 1 : 0, sizeof(WoRun));
   size_t o = 0;
   for (int b = 0; b < mpc_plan::B_COUNT; ++b) {
     o = (o + 255) & ~(size_t)255;
@@ -3798,7 +4180,8 @@ int mpc_plan_workspace_bytes(const mpc_plan* p, size_t* bytes) {
 
 int mpc_plan_set_input(mpc_plan* p, const mpc_input* in) {
   if (!p || !in) return fail(MPC_E_ARG, "null argument");
-  if (in->n_reads != p->N || in->n_samples != p->S || in->cs_bytes > p->in.cs_bytes)
+  if (in->n_reads != p->N || in->n_samples != p->S || in->cs_bytes > p->in.cs_bytes ||
+      (in->neg_reads > 0) != (p->in.neg_reads > 0))  // (the K_parse the plan bound; the list capacity stays)
     return fail(MPC_E_ARG, "input shape differs from the plan");
   p->in = *in;
   p->in.h_cs_off = nullptr;  // the work split stays the one planned
@@ -3827,7 +4210,7 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
   if (!p->work_subsum.empty())
     HIPCHK(hipMemcpy(at<int32_t>(p, mpc_plan::B_WSUBSUM), p->work_subsum.data(), 4 * p->work_subsum.size(),
                      hipMemcpyHostToDevice));
-  HIPCHK(hipFuncSetAttribute(parse_kernel(p->tally_mode, p->parse_win), hipFuncAttributeMaxDynamicSharedMemorySize,
+  HIPCHK(hipFuncSetAttribute(parse_kernel(p), hipFuncAttributeMaxDynamicSharedMemorySize,
                              p->parse_lds));
   p->bound = true;
   p->runt_dirty = true;
@@ -3962,7 +4345,13 @@ int mpc_layout(mpc_plan* p, void* stream) {
   NEED_BOUND(p);
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
-  hipLaunchKernelGGL(K_layout, dim3(nblk(p->G, kGB)), dim3(kGB), 0, st, d, next_epoch());
+  if (p->wo_cap > 0) {  // negative starts: the wrapped odd positions first
+    hipLaunchKernelGGL(K_woprep, dim3(1), dim3(1024), 0, st, d);
+    if (p->N > 0) hipLaunchKernelGGL(K_wocover, dim3(nblk(p->N, 256)), dim3(256), 0, st, d);
+    hipLaunchKernelGGL(K_layout<true>, dim3(nblk(p->G, kGB)), dim3(kGB), 0, st, d, next_epoch());
+  } else {
+    hipLaunchKernelGGL(K_layout<false>, dim3(nblk(p->G, kGB)), dim3(kGB), 0, st, d, next_epoch());
+  }
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }
@@ -3975,6 +4364,7 @@ int mpc_rows(mpc_plan* p, void* stream) {
   HIPCHK(hipGetLastError());
   p->runt_dirty = false;  // K_ins (enqueued) zeroes every run tally it maps (all runs of all gaps)
   if (p->N > 0) launch_flank(p, d, st);
+  if (p->wo_cap > 0) hipLaunchKernelGGL(K_worows, dim3(64), dim3(256), 0, st, d);
   HIPCHK(hipGetLastError());
   return MPC_OK;
 }

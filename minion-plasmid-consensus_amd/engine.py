@@ -7,6 +7,7 @@ is missing, :class:`Engine` raises.
 """
 import ctypes
 import os
+import warnings
 
 import numpy as np
 
@@ -14,8 +15,9 @@ from . import _build
 
 LIB_PATH = _build.LIBMPC
 
-ABI_VERSION = 7
+ABI_VERSION = 8
 MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED, MPC_ST_RSORT_PATH = 0, 1, 2, 3, 5
+MPC_ST_WRAP_EVENTS, MPC_ST_WRAP_POS = 6, 7
 DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL, DE_UNSUPPORTED = 1, 2, 4, 8, 16, 32, 64
 (BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_CNT, BUF_RIGHT_CNT_ALL,
  BUF_HASLEFT, BUF_MAXR, BUF_RUN_M, BUF_RUN_R, BUF_DIFF, BUF_SUB) = range(14)
@@ -23,7 +25,8 @@ PHASES = ("parse", "index", "runs", "tally", "layout", "rows")
 
 DE_NAMES = {DE_OP: "Unknown operator", DE_VALUE: "ValueError", DE_INDEX: "IndexError", DE_KEY: "KeyError",
             DE_CAPACITY: "row capacity", DE_INTERNAL: "internal invariant",
-            DE_UNSUPPORTED: "unsupported input (a negative target start writing into a wrapped odd position)"}
+            DE_UNSUPPORTED: "unsupported input (a negative target start the plan was not sized for, or an "
+                            "advance of 2^22 or more from a negative coordinate)"}
 K_PARSE, K_ODD, K_LEFT, K_FLANK, K_INS, K_RSORT = 0, 1, 2, 3, 4, 5
 CS_PAD = 2048  # readable bytes required past the end of the cs buffer (mpc.h)
 FLANK_PAD = 16  # readable bytes required past the end of the up/down buffers (mpc.h)
@@ -76,6 +79,8 @@ class _Input(ctypes.Structure):
         ("n_shards", ctypes.c_int32),
         ("h_cs_off", ctypes.POINTER(ctypes.c_int64)),
         ("parse_cus", ctypes.c_int32),
+        ("neg_reads", ctypes.c_int64),
+        ("neg_cs_bytes", ctypes.c_int64),
     ]
 
 
@@ -331,13 +336,23 @@ class Batch:
             raise MpcError("target start out of int32 range")
         sample = np.repeat(np.arange(S, dtype=np.int32), counts)
         self.cs_bytes = int(cs_off[-1])
+        # reads with a negative target start (Python's negative wrap, mpc.h): they
+        # size the plan's list of strings written into wrapped odd positions
+        neg = tstart < 0
+        self.neg_reads = int(neg.sum())
+        self.neg_cs_bytes = int((cs_off[1:] - cs_off[:-1])[neg].sum()) if self.neg_reads else 0
         self.aligned_bases = int(sum(int(np.asarray(s.get("aligned", [0])).sum()) for s in samples))
 
         def dev(a, pad=0):
             a = np.ascontiguousarray(a)
             t = torch.empty(max(a.nbytes + pad, 16), dtype=torch.uint8, device=self.device)
             if a.nbytes:
-                t[: a.nbytes].copy_(torch.from_numpy(a.view(np.uint8).reshape(-1)))
+                # (read-only views of the ingest's buffers are only read here: the
+                # host tensor is the source of one H2D copy, never written)
+                with warnings.catch_warnings():
+                    warnings.filterwarnings("ignore", message="The given NumPy array is not writable")
+                    h = torch.from_numpy(a.view(np.uint8).reshape(-1))
+                t[: a.nbytes].copy_(h)
             if pad:
                 t[a.nbytes:].zero_()
             return t
@@ -368,7 +383,7 @@ class Batch:
             shard=self.shard, n_shards=self.n_shards,
             h_cs_off=(self._keep[2].ctypes.data_as(ctypes.POINTER(ctypes.c_int64)) if self.balance_bytes
                       else ctypes.POINTER(ctypes.c_int64)()),
-            parse_cus=int(self.parse_cus),
+            parse_cus=int(self.parse_cus), neg_reads=self.neg_reads, neg_cs_bytes=self.neg_cs_bytes,
         )
 
     def row_estimate(self):

@@ -31,8 +31,8 @@
  * (obs_index): a negative target start (never written by minimap2) reaches
  * refarr / obsarr at len + index, like the reference (:222, :300-303, :57-61,
  * :69, :79, :87, :96), pinned by tests/golden/n_neg_*.  The HIP path
- * implements the part of it that keeps odd positions single-slot and rejects
- * the rest (MPC_DE_UNSUPPORTED, include/mpc.h).
+ * implements all of it on one shard, including the strings the wrap writes
+ * into odd positions (K_woprep .. K_worows, include/mpc.h).
  */
 #include <stdint.h>
 #include <stdlib.h>

@@ -5,16 +5,11 @@ import os
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
-# Documented divergences of the HIP path from the reference (DESIGN.md §6,
-# include/mpc.h MPC_DE_UNSUPPORTED): a negative target start whose flank or
-# '+' insertion Python's negative index wrap writes into an ODD position (extra
-# slots in a reference-base position).  The reference exits 0 (the golden pins
-# what it writes; the oracle matches it); the drop-in exits 1 with no outputs.
-DIVERGENT = {
-    "n_neg_ins": "'+' at a negative coordinate in [-n, 0): slots in wrapped odd position n + i",
-    "n_neg_flank": "upstream flank at a negative tstart in [-n, 0): slots in wrapped odd position n + tstart",
-    "n_neg_end": "downstream flank of a read ending in [-n, 0): slots appended to a wrapped odd position",
-}
+# Documented divergences of the HIP path from the reference.
+# Empty since round 6: the three negative-target-start cases whose strings
+# Python's negative index wrap writes into an ODD position (n_neg_ins,
+# n_neg_flank, n_neg_end) are replayed on the device (K_woprep .. K_worows).
+DIVERGENT = {}
 
 
 def cases():

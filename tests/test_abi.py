@@ -30,7 +30,7 @@ def test_library_exports_all(pkg):
     for name in declared():
         assert hasattr(lib, name), name
     lib.mpc_version.restype = ctypes.c_int
-    assert lib.mpc_version() == pkg.engine.ABI_VERSION == 7
+    assert lib.mpc_version() == pkg.engine.ABI_VERSION == 8
 
 
 def test_no_oracle_in_product():
@@ -173,7 +173,7 @@ def test_input_struct_layout(pkg):
     off = (ctypes.c_size_t * n)()
     size = L.mpc_input_layout(off, n)
     assert size == ctypes.sizeof(e._Input)
-    assert n == 22  # MPC_INPUT_FIELDS
+    assert n == 24  # MPC_INPUT_FIELDS
     for k, (name, _) in enumerate(e._Input._fields_):
         assert off[k] == getattr(e._Input, name).offset, name
     assert _integration_fields() == [f for f, _ in e._Input._fields_]

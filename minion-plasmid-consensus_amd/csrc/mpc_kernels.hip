@@ -206,6 +206,7 @@ constexpr int64_t kWoCapMax = 1 << 22;  // event list bound (the single-workgrou
 constexpr int kPgEv = 64;                    // events per page (256 B)
 constexpr int kPgBits = 12;                  // bucket word: page << 12 | fill
 constexpr uint32_t kPgNone = 0xFFFFFu;       // page field of a bucket with no page yet
+constexpr uint32_t kPgOvf = kPgNone - 1u;    // ... of a bucket whose workgroup ran out of pages (DE_INTERNAL)
 constexpr uint32_t kPgInit = (kPgNone << kPgBits) | (uint32_t)kPgEv;  // first event opens a page
 constexpr uint32_t kPgMark = 0xFFFFFFFFu;    // pg_own of a bucket's last page (placed by the epilogue)
 static_assert(kPgEv + 1024 < (1 << kPgBits), "fill field: a full page plus every thread of a block waiting");
@@ -715,18 +716,25 @@ __device__ __forceinline__ void parse_place_event(const ParseArgs& a, bool has, 
       if (!first) old = atomicAdd(W, 1u);
       first = false;
       const uint32_t slot = old & ((1u << kPgBits) - 1u), pg = old >> kPgBits;
-      if (slot < (uint32_t)kPgEv) {
+      if (pg == kPgOvf && slot > (uint32_t)kPgEv) {
+        // the region ran out of pages (flagged by the opener): the event is
+        // dropped, and the word reset so its fill never carries into the page field
+        atomicExch(W, (kPgOvf << kPgBits) | (uint32_t)kPgEv);
+        need = false;
+      } else if (slot < (uint32_t)kPgEv) {
         pg0[pg * kPgEv + slot] = word;
         need = false;
       } else if (slot == (uint32_t)kPgEv) {
-        uint32_t np = atomicAdd(npg, 1u);
+        const uint32_t np = atomicAdd(npg, 1u);
         if (np >= pcap) {  // never expected: the page region bound (parse_page_base)
+          // publish the overflow page, so waiting lanes leave (dropping their events)
           atomicOr(&a.status[MPC_ST_FLAGS], DE_INTERNAL);
-          np = pcap - 1;
+          atomicExch(W, (kPgOvf << kPgBits) | (uint32_t)kPgEv);
+        } else {
+          a.pg_own[pbase + np] = (uint32_t)b;
+          pg0[np * kPgEv] = word;
+          atomicExch(W, (np << kPgBits) | 1u);
         }
-        a.pg_own[pbase + np] = (uint32_t)b;
-        pg0[np * kPgEv] = word;
-        atomicExch(W, (np << kPgBits) | 1u);
         need = false;
       } else {
         waiting = true;  // the page filled meanwhile: wait for its opener
@@ -747,7 +755,7 @@ __device__ __forceinline__ void parse_place_event(const ParseArgs& a, bool has, 
 // thread of the block calls it.
 template <int TM>
 __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, uint32_t* hl, uint32_t* W, uint32_t* uni,
-                               const uint32_t* npg, int64_t pbase) {
+                               const uint32_t* npg, int64_t pbase, uint32_t pcap) {
   constexpr bool big = TM == 4;
   constexpr bool fused = TM >= 1 && TM <= 3;
   constexpr bool lds_sub = TM == 1 || TM == 2;
@@ -788,11 +796,11 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, uint3
     return big ? __hip_atomic_load(W + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : W[b];
   };
   __syncthreads();  // (LDS tallies flushed: cnt / cur may alias them)
-  const uint32_t np_all = *npg;
+  const uint32_t np_all = min(*npg, pcap);  // (the counter runs past pcap only after DE_INTERNAL)
   // A: mark every bucket's last page (it goes to the end of the bucket's list)
   for (int b = threadIdx.x; b < nbk; b += blockDim.x) {
     const uint32_t w = wload(b);
-    if ((w >> kPgBits) != kPgNone) a.pg_own[pbase + (w >> kPgBits)] = kPgMark;
+    if ((w >> kPgBits) < pcap) a.pg_own[pbase + (w >> kPgBits)] = kPgMark;
     if (!big) cnt[b] = 0;
   }
   __syncthreads();
@@ -813,7 +821,7 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, uint3
         w = wload(b);
         c = big ? (uint32_t)__hip_atomic_load(cnt + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : cnt[b];
       }
-      const bool has = (w >> kPgBits) != kPgNone;
+      const bool has = (w >> kPgBits) < pcap;  // (not kPgNone, not kPgOvf)
       const int np = (int)c + (has ? 1 : 0);
       const int inc = wave_scan_i32(np);
       const int off = carry + inc - np;
@@ -888,7 +896,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   // the workgroup's page region [pbase, pnext) (parse_page_base)
   const int64_t pbase = parse_page_base(a.cs_off[r0] - a.cs_base, r0, blockIdx.x, a.nbs);
   const int64_t pnext = parse_page_base(a.cs_off[r1] - a.cs_base, r1, blockIdx.x + 1, a.nbs);
-  const uint32_t pcap = (uint32_t)min(pnext - pbase, (int64_t)kPgNone);
+  const uint32_t pcap = (uint32_t)min(pnext - pbase, (int64_t)kPgOvf);
   uint32_t* const pg0 = a.ins_sorted + pbase * kPgEv;  // the region's first event slot
   constexpr bool fused = TM >= 1 && TM <= 3;  // depth differences in LDS (one address space per instantiation)
   constexpr bool lds_sub = TM == 1 || TM == 2;  // substitution tallies in LDS too
@@ -1473,7 +1481,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   if (parse_dma<WIN>()) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   MPC_SEG(6);
-  parse_epilogue<TM>(a, n, gb, nbk, hl, bkw, uni, npg, pbase);
+  parse_epilogue<TM>(a, n, gb, nbk, hl, bkw, uni, npg, pbase, pcap);
 #ifdef MPC_STAMPS
   MPC_SEG(7);
   const int64_t gw = (int64_t)blockIdx.x * kMaxPW + w;

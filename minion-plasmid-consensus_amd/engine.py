@@ -103,31 +103,42 @@ def _hip_runtime_paths():
 
 def _elf_dynamic(path):
     """(SONAME, [NEEDED...]) of an ELF64 little-endian shared library, from its
-    .dynamic section (no tools, no loading); (None, []) if unreadable."""
+    .dynamic section (no tools, no loading; only the ELF header, the section
+    headers and the .dynamic / string-table ranges are read); (None, []) if
+    unreadable."""
     import struct
     try:
         with open(path, "rb") as f:
-            data = f.read()
-        if data[:4] != b"\x7fELF" or data[4] != 2 or data[5] != 1:
-            return None, []
-        shoff, = struct.unpack_from("<Q", data, 0x28)
-        shentsize, shnum = struct.unpack_from("<HH", data, 0x3A)
-        secs = [struct.unpack_from("<IIQQQQIIQQ", data, shoff + k * shentsize) for k in range(shnum)]
-        dyn = next((sh for sh in secs if sh[1] == 6), None)  # SHT_DYNAMIC
-        if dyn is None:
-            return None, []
-        strtab = secs[dyn[6]]  # sh_link: its string table
-        sname = lambda o: data[strtab[4] + o: data.index(b"\0", strtab[4] + o)].decode()
-        soname, needed = None, []
-        for k in range(dyn[5] // 16):
-            tag, val = struct.unpack_from("<qQ", data, dyn[4] + 16 * k)
-            if tag == 0:
-                break
-            if tag == 14:
-                soname = sname(val)
-            elif tag == 1:
-                needed.append(sname(val))
-        return soname, needed
+            def at(off, n):
+                f.seek(off)
+                b = f.read(n)
+                if len(b) != n:
+                    raise ValueError("short read")
+                return b
+            hdr = at(0, 64)
+            if hdr[:4] != b"\x7fELF" or hdr[4] != 2 or hdr[5] != 1:
+                return None, []
+            shoff, = struct.unpack_from("<Q", hdr, 0x28)
+            shentsize, shnum = struct.unpack_from("<HH", hdr, 0x3A)
+            sh = at(shoff, shentsize * shnum)
+            secs = [struct.unpack_from("<IIQQQQIIQQ", sh, k * shentsize) for k in range(shnum)]
+            dyn = next((x for x in secs if x[1] == 6), None)  # SHT_DYNAMIC
+            if dyn is None:
+                return None, []
+            strtab = secs[dyn[6]]  # sh_link: its string table
+            strs = at(strtab[4], strtab[5])
+            dynb = at(dyn[4], dyn[5])
+            sname = lambda o: strs[o: strs.index(b"\0", o)].decode()
+            soname, needed = None, []
+            for k in range(len(dynb) // 16):
+                tag, val = struct.unpack_from("<qQ", dynb, 16 * k)
+                if tag == 0:
+                    break
+                if tag == 14:
+                    soname = sname(val)
+                elif tag == 1:
+                    needed.append(sname(val))
+            return soname, needed
     except (OSError, ValueError, struct.error, IndexError, StopIteration, UnicodeDecodeError):
         return None, []
 
@@ -151,20 +162,18 @@ def _preload_hip_runtime():
     binds libmpc.so's dependency to it by SONAME, and a later ``import torch``
     finds the same file already mapped -- one runtime in either import order.
     When the SONAMEs differ (a PyTorch built against another HIP major) the
-    two cannot be shared: initialise PyTorch first so that its runtime is the
-    one in use, and report both names if a second runtime gets mapped anyway.
-    Without PyTorch (a C-ABI user) the system ROCm copy is used.  Returns
-    (torch's SONAME, libmpc's NEEDED HIP runtime) for the error message."""
+    two cannot be shared: raise before anything is loaded or initialised
+    (loading libmpc.so would map a second runtime).  Without PyTorch (a C-ABI
+    user) the system ROCm copy is used."""
     path = _torch_hip_runtime()
     if path is None:
-        return None, None
+        return
     torch_so, _ = _elf_dynamic(path)
     need = next((x for x in _elf_dynamic(LIB_PATH)[1] if x.startswith("libamdhip64.so")), None)
     if torch_so is not None and need is not None and torch_so != need:
-        _torch().cuda.is_available()  # PyTorch's runtime first (the pre-round-4 order)
-        return torch_so, need
+        raise MpcError("libmpc.so needs %s but PyTorch ships %s: two HIP runtimes cannot share this process; "
+                       "rebuild libmpc.so against PyTorch's HIP" % (need, torch_so))
     ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
-    return torch_so, need
 
 
 def lib():
@@ -172,13 +181,10 @@ def lib():
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             raise MpcError(f"{LIB_PATH} is missing: build it with __graft_entry__.build() (no CPU fallback)")
-        torch_so, need = _preload_hip_runtime()
+        _preload_hip_runtime()
         L = ctypes.CDLL(LIB_PATH)
         rt = _hip_runtime_paths()
         if len(rt) > 1:
-            if torch_so != need:
-                raise MpcError("libmpc.so needs %s but PyTorch ships %s: two HIP runtimes are mapped (%s); "
-                               "rebuild libmpc.so against PyTorch's HIP" % (need, torch_so, ", ".join(sorted(rt))))
             raise MpcError("two HIP runtimes are mapped into this process (%s): load libmpc.so through "
                            "engine.lib() before anything else loads a HIP runtime" % ", ".join(sorted(rt)))
         vp, i64, i32, dbl = ctypes.c_void_p, ctypes.c_int64, ctypes.c_int, ctypes.c_double

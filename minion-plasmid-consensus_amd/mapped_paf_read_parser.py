@@ -166,6 +166,9 @@ def main(argv=None, timings=None):
     except (ingest.IngestError, engine.DataError, OSError, UnicodeDecodeError) as e:
         print("Error: {}".format(e), file=sys.stderr)
         return 1
+    except engine.MpcError as e:  # input past the engine's limits (e.g. a reference over 2^22 - 2 bases)
+        print("Error: {}".format(e), file=sys.stderr)
+        return 1
     t2 = time.perf_counter()
     for (ref, paf, _, c, ch, acc), res in zip(jobs, results):
         statprint("Max depth is {}.".format(res["max_depth"]))

@@ -281,10 +281,56 @@ def negative_cases(script):
               "a read ending below 0 with a downstream flank: slots appended to a wrapped odd position")
 
 
+def long_reference_cases(script):
+    """A reference one base past the engine's coordinate limit (include/mpc.h:
+    n <= 2^22 - 2 = 4,194,302; the reference takes any length, :161-184), with
+    a handful of reads at its start, middle and end.  The reference exits 0;
+    the drop-in rejects the plan and exits 1 (tests/golden_util.py DIVERGENT).
+    The sequence repeats a 1020-base unit with a few point changes, so the
+    gzip'd fixture stays small."""
+    import random
+    rng = random.Random(22)
+    n = (1 << 22) - 1
+    unit = "".join(rng.choice("ACGT") for _ in range(1020))  # 17 lines of 60: gzip sees the repeats
+    ref = list((unit * (n // 1020 + 1))[:n])
+    for k in range(40):
+        ref[rng.randrange(n)] = rng.choice("ACGT")
+    ref = "".join(ref)
+    R = ">big\n" + "\n".join(ref[i:i + 60] for i in range(0, n, 60)) + "\n"
+    reads, paf = [], []
+
+    def add(name, ts, cs_ops, up, down):
+        # query = upstream + aligned bases (matches copy the reference, '*' y, '+' s) + downstream
+        q, i = [up], ts
+        for op, v in cs_ops:
+            if op == ":":
+                q.append(ref[i:i + v]); i += v
+            elif op == "*":
+                q.append(v[1].upper()); i += 1
+            elif op == "+":
+                q.append(v.upper())
+            elif op == "-":
+                i += len(v)
+        q.append(down)
+        seq = "".join(q)
+        cs = "".join(op + (str(v) if op == ":" else v) for op, v in cs_ops)
+        reads.append(">%s\n%s\n" % (name, seq))
+        paf.append(paf_line(name, len(seq), len(up), len(seq) - len(down), "+", ts, i, cs))
+
+    add("r1", 0, [(":", 120), ("*", "ag"), (":", 40)], "", "TTGCA")
+    add("r2", 2_097_000, [(":", 60), ("+", "tta"), (":", 30), ("-", "ac"), (":", 70)], "GGA", "CAT")
+    add("r3", 2_097_010, [(":", 200)], "AC", "")
+    add("r4", n - 150, [(":", 80), ("*", "ct"), (":", 69)], "ACGTT", "GATTACA")
+    add("r5", n - 100, [(":", 100)], "", "CCCC")
+    emit_case(script, "l_ref_past_limit", R, "".join(reads), "".join(paf), [(0.1, 5), (0, 1)],
+              "reference of 2^22 - 1 bases, one past the engine's coordinate limit")
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--ref-script", default="/root/reference/src/mapped_paf_read_parser.py")
-    ap.add_argument("--only", default="", help="'unicode' / 'negative': regenerate only the non-ASCII / negative-tstart cases")
+    ap.add_argument("--only", default="", help="'unicode' / 'negative' / 'long': regenerate only the non-ASCII / negative-tstart / "
+                                            "past-the-length-limit cases")
     a = ap.parse_args()
     os.makedirs(GOLDEN, exist_ok=True)
     if a.only == "unicode":
@@ -293,9 +339,13 @@ def main():
     if a.only == "negative":
         negative_cases(a.ref_script)
         return
+    if a.only == "long":
+        long_reference_cases(a.ref_script)
+        return
     hand_cases(a.ref_script)
     unicode_cases(a.ref_script)
     negative_cases(a.ref_script)
+    long_reference_cases(a.ref_script)
     random_cases(a.ref_script)
 
 

@@ -6,10 +6,15 @@ import os
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
 
 # Documented divergences of the HIP path from the reference.
-# Empty since round 6: the three negative-target-start cases whose strings
-# Python's negative index wrap writes into an ODD position (n_neg_ins,
-# n_neg_flank, n_neg_end) are replayed on the device (K_woprep .. K_worows).
-DIVERGENT = {}
+# Since round 6 the three negative-target-start cases whose strings Python's
+# negative index wrap writes into an ODD position (n_neg_ins, n_neg_flank,
+# n_neg_end) are replayed on the device (K_woprep .. K_worows) and match.
+# What remains: references past the engine's coordinate scheme (include/mpc.h,
+# n <= 2^22 - 2).  The reference exits 0 (the golden pins what it writes; the
+# oracle matches it); the drop-in exits 1 with no outputs.
+DIVERGENT = {
+    "l_ref_past_limit": "reference of 2^22 - 1 bases: past the 32-bit coordinate scheme (mpc_plan_create MPC_E_ARG)",
+}
 
 
 def cases():

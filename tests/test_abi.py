@@ -220,26 +220,32 @@ def test_product_build_flags(pkg):
 
 
 def test_hip_runtime_soname_check(pkg, monkeypatch):
-    """ADVICE r04: the torch-first preload compares SONAMEs.  Same SONAME ->
+    """ADVICE r04/r05: the torch-first preload compares SONAMEs.  Same SONAME ->
     map PyTorch's copy by path; a different one (PyTorch on another HIP major)
-    -> initialise PyTorch first instead, and name both in the error."""
+    -> MpcError naming both, raised before libmpc.so is loaded and without
+    initialising any HIP runtime."""
     e = pkg.engine
     need = [x for x in e._elf_dynamic(e.LIB_PATH)[1] if x.startswith("libamdhip64.so")]
     assert len(need) == 1
     tpath = e._torch_hip_runtime()
     if tpath is not None:
         assert e._elf_dynamic(tpath)[0].startswith("libamdhip64.so")
-    seen = []
     monkeypatch.setattr(e, "_torch_hip_runtime", lambda: "/x/libamdhip64.so")
     monkeypatch.setattr(e, "_elf_dynamic", lambda p: ("libamdhip64.so.9", []) if p.startswith("/x/")
                         else (None, ["libamdhip64.so.7"]))
+    monkeypatch.setattr(e, "_torch", lambda: pytest.fail("torch must not be touched"))
+    monkeypatch.setattr(e.ctypes, "CDLL", lambda *a, **k: pytest.fail("nothing may be loaded"))
+    with pytest.raises(e.MpcError) as err:
+        e._preload_hip_runtime()
+    assert "libamdhip64.so.9" in str(err.value) and "libamdhip64.so.7" in str(err.value)
 
-    class T:
-        class cuda:
-            @staticmethod
-            def is_available():
-                seen.append("torch first")
-                return False
-    monkeypatch.setattr(e, "_torch", lambda: T)
-    assert e._preload_hip_runtime() == ("libamdhip64.so.9", "libamdhip64.so.7")
-    assert seen == ["torch first"]
+
+def test_elf_dynamic_reads_ranges(tmp_path):
+    """_elf_dynamic parses the real libraries and rejects a truncated file."""
+    import importlib
+    e = importlib.import_module("minion-plasmid-consensus_amd.engine")
+    so, need = e._elf_dynamic(e.LIB_PATH)
+    assert any(x.startswith("libamdhip64.so") for x in need)
+    cut = tmp_path / "cut.so"
+    cut.write_bytes(open(e.LIB_PATH, "rb").read(200))
+    assert e._elf_dynamic(str(cut)) == (None, [])

@@ -33,6 +33,10 @@ def test_cli_matches_reference(case, tmp_path, cli):
         rc = cli.main(["--ref", ref, "--reads", reads, "--paf", paf, "--consensus", outs[0], "--chromat", outs[1],
                        "--accuracies", outs[2], "--min_depth_factor", repr(run["mdf"]),
                        "--global_threshold_factor", repr(run["gtf"])])
+        if case in gu.DIVERGENT:  # pinned divergence: the reference writes files, the drop-in rejects
+            assert run["exit"] == 0 and rc == 1, (case, k, gu.DIVERGENT[case])
+            assert not any(os.path.exists(o) for o in outs)
+            continue
         assert rc == run["exit"], (case, k)
         if rc == 0:
             for o, f in zip(outs, ("c.fa", "ch.tsv", "acc.tsv")):

@@ -53,7 +53,7 @@
 #endif
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
-    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES)
+    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -92,6 +92,10 @@ constexpr uint32_t kNullGap = 0x3fffffu;
 // (1 = a block's own sum, 2 = its inclusive prefix), the launch epoch in bits
 // 32-61, the 32-bit value below
 constexpr uint64_t kSelAgg = 1ull << 62, kSelPre = 2ull << 62, kSelTag = 0x3fffffffull << 32;
+// look-back predecessors per lane and step (1: 64 per step)
+#ifndef MPC_LOOKBACK_U
+#define MPC_LOOKBACK_U 1
+#endif
 
 // Decoupled look-back, called by ONE wave of block b: publishes the block's NV
 // values (own[k], flag 1), sums its predecessors' values back to the nearest
@@ -636,11 +640,39 @@ struct WinIn {
   uint32_t uo, dno;  // low words of the flank offsets: only the lengths' signs are needed
   int32_t ts;
 };
+// A lane's cs bytes of a window.  The cs stream is read exactly once:
+// MPC_CS_NT loads it non-temporally (evict-first in the caches), so it does not
+// push the insertion pages being filled out of L2 before their lines are whole.
+#ifndef MPC_CS_NT
+#define MPC_CS_NT 1
+#endif
+typedef unsigned int u32x4_t __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint4 nt_load16(const uint8_t* p) {
+  const u32x4_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x4_t*>(p));
+  return make_uint4(v.x, v.y, v.z, v.w);
+}
+template <int CH>
+__device__ __forceinline__ typename Chunk<CH>::T cs_load(const uint8_t* p) {
+  if constexpr (!MPC_CS_NT) {
+    return *reinterpret_cast<const typename Chunk<CH>::T*>(p);
+  } else if constexpr (CH == 32) {
+    U8x32 v;
+    v.a = nt_load16(p);
+    v.b = nt_load16(p + 16);
+    return v;
+  } else if constexpr (CH == 16) {
+    return nt_load16(p);
+  } else {
+    const u32x2_t v = __builtin_nontemporal_load(reinterpret_cast<const u32x2_t*>(p));
+    return make_uint2(v.x, v.y);
+  }
+}
 template <int CH, bool DATA = true>
 __device__ __forceinline__ WinIn<CH> fetch_window(const ParseArgs& a, int64_t P, int64_t rs0, int l) {
   WinIn<CH> f;
   const int64_t A = P & ~(int64_t)15;
-  if (DATA) f.d = *reinterpret_cast<const typename Chunk<CH>::T*>(a.cs + A + CH * l);
+  if (DATA) f.d = cs_load<CH>(a.cs + A + CH * l);
   const int64_t r = rs0 + l;
   const bool ok = r <= a.n_reads;
   f.o = ok ? a.cs_off[r] : INT64_MAX;
@@ -2108,32 +2140,42 @@ __global__ __launch_bounds__(256) void K_rstart(Dev d) {
   }
 }
 
-// Several shards: global right_start and roff from all shards' per-gap counts
-// (one workgroup, block scan over the gaps).
-__global__ __launch_bounds__(1024) void K_runs(Dev d) {
-  __shared__ int32_t s_w[16];
-  __shared__ int32_t s_carry;
-  if (threadIdx.x == 0) s_carry = 0;
-  __syncthreads();
+// Several shards: global right_start and roff from all shards' per-gap counts:
+// 1024 gaps per block, the blocks' sums chained by a decoupled look-back
+// (K_layout's status words, which it re-tags with its own epoch later in the
+// step; one workgroup over all gaps took C2 x 8 shards 18 us)
+constexpr int kRunsGB = 1024;
+__global__ __launch_bounds__(kRunsGB) void K_runs(Dev d, uint32_t epoch) {
+  __shared__ int32_t s_w[kRunsGB / 64];
+  __shared__ int64_t s_pre;
   const int l = lane(), w = threadIdx.x >> 6;
-  for (int64_t c0 = 0; c0 <= d.G; c0 += blockDim.x) {
-    const int64_t g = c0 + threadIdx.x;
-    int32_t tot = 0, below = 0;
-    if (g < d.G)
-      for (int k = 0; k < d.n_shards; ++k) {
-        const int32_t c = d.rcnt_all[(int64_t)k * d.G + g];
-        tot += c;
-        if (k < d.shard) below += c;
-      }
-    const int inc = wave_scan_i32(tot);
-    if (l == 63) s_w[w] = inc;
-    __syncthreads();
-    int pre = s_carry;
-    for (int k = 0; k < w; ++k) pre += s_w[k];
-    if (g <= d.G) { d.right_start[g] = pre + inc - tot; d.roff[g] = below; }
-    __syncthreads();
-    if (threadIdx.x == blockDim.x - 1) s_carry = pre + inc;
-    __syncthreads();
+  const int64_t b = blockIdx.x;
+  const int64_t g = b * kRunsGB + threadIdx.x;
+  int32_t tot = 0, below = 0;
+  if (g < d.G)
+    for (int k = 0; k < d.n_shards; ++k) {
+      const int32_t c = d.rcnt_all[(int64_t)k * d.G + g];
+      tot += c;
+      below += k < d.shard ? c : 0;
+    }
+  const int inc = wave_scan_i32(tot);
+  if (l == 63) s_w[w] = inc;
+  __syncthreads();
+  int32_t wpre = 0, bt = 0;
+  for (int k = 0; k < kRunsGB / 64; ++k) {
+    wpre += k < w ? s_w[k] : 0;
+    bt += s_w[k];
+  }
+  if (w == 0) {
+    int64_t pre;
+    lookback<1, MPC_LOOKBACK_U>(reinterpret_cast<uint64_t*>(d.bsum), b, (uint64_t)(epoch & 0x3fffffffu) << 32, &bt, &pre,
+                                &d.status[MPC_ST_FLAGS]);
+    if (l == 0) s_pre = pre;
+  }
+  __syncthreads();
+  if (g <= d.G) {
+    d.right_start[g] = (int32_t)(s_pre + wpre + inc - tot);
+    d.roff[g] = below;
   }
 }
 
@@ -2433,8 +2475,8 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       // LDS runs this unit can touch: an event at gap p has run k in
       // [roff, roff + its mixed RIGHT reads]; the flush covers runs < s_kn
       if (threadIdx.x < kBW && (int)threadIdx.x <= uv.gl - g0) {
-        const int p = (int)threadIdx.x, k0 = s_roff[p];
-        if (k0 < kKMax) atomicMax(&s_kn, min(k0 + s_rsl[p + 1] - s_rsl[p], kKMax - 1) + 1);
+        const int p = (int)threadIdx.x;
+        atomicMax(&s_kn, min(s_rsl[p + 1] - s_rsl[p], kKMax - 1) + 1);
       }
     }
     MPC_LSEG(2);
@@ -2450,7 +2492,9 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       const int L = (int)((ev >> 8) & 3u) + 1;
       const int p = gap - g0;
       const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
-      int32_t k = s_roff[p];  // run of the event within its gap
+      // run of the event within its gap: this shard's runs of the gap start at
+      // roff (the RIGHT events of lower shards); k counts from there
+      int32_t k = 0;
       if (lb > la) {
         if (vl) {  // 32-bit search of the staged RIGHT reads
           int lo = la - v0, hi = lb - v0;
@@ -2466,6 +2510,8 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       }
       // the bases too, run-relative (LEFT: base bi from the 3' end lands on the
       // run's slot hi_run - 1 - bi, :37-62): K_ins maps them to rows after the layout
+      // LDS slots: the shard's runs of the gap (as many as on one GPU); the
+      // global run is s_rs[p] + g + roff + k
       if (k < kKMax) {
         // the run's longest LEFT string: UB = 1024 takes it from the highest
         // slot holding a base at the flush (one LDS atomic less per event: C4
@@ -2476,8 +2522,9 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
         for (int j = 0; j < kInsInline; ++j)  // straight-line: bases j < L
           if (j < L) atomicAdd(tp + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
       } else {
-        atomicMax(a.M + s_rs[p] + g + (int64_t)k, L);
-        uint32_t* rt = a.runt + (s_rs[p] + g + (int64_t)k) * 16;
+        const int64_t run = s_rs[p] + g + (int64_t)s_roff[p] + k;
+        atomicMax(a.M + run, L);
+        uint32_t* rt = a.runt + run * 16;
         for (int j = 0; j < L; ++j) atomicAdd(rt + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);
       }
     }
@@ -2490,7 +2537,7 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
         const int p = q & (kBW - 1), k = q / kBW;
         const uint32_t m = Ml[p * kMs + k];
         if (m) {
-          atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + k, (int32_t)m);
+          atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + s_roff[p] + k, (int32_t)m);
           Ml[p * kMs + k] = 0;
         }
       }
@@ -2498,7 +2545,7 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
         const int p = (q >> 4) & (kBW - 1), k = q / (kBW * 16);
         const uint32_t v = Tl[p * kTs + k * 16 + (q & 15)];
         if (v) {
-          atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + k) * 16 + (q & 15), v);
+          atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + s_roff[p] + k) * 16 + (q & 15), v);
           Tl[p * kTs + k * 16 + (q & 15)] = 0;
         }
       }
@@ -2510,7 +2557,7 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       const int k = (q >> 4) % kKMax, p = (q >> 4) / kKMax;
       const uint32_t v = Tl[p * kTs + k * 16 + (q & 15)];
       if (v) {
-        atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + k) * 16 + (q & 15), v);
+        atomicAdd(a.runt + (s_rs[p] + (int64_t)gb + g0 + p + s_roff[p] + k) * 16 + (q & 15), v);
         atomicMax(&Ml[p * kMs + k], (uint32_t)((q & 15) >> 2) + 1u);  // slot bi holds a base: M > bi
       }
     }
@@ -2518,7 +2565,7 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     for (int q = threadIdx.x; q < kBW * kKMax; q += blockDim.x) {
       const int k = q % kKMax, p = q / kKMax;
       const uint32_t m = Ml[p * kMs + k];
-      if (m) atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + k, (int32_t)m);
+      if (m) atomicMax(a.M + s_rs[p] + (int64_t)gb + g0 + p + s_roff[p] + k, (int32_t)m);
     }
     __syncthreads();
     MPC_LSEG(6);
@@ -2793,9 +2840,6 @@ __device__ void wo_cover_read(const Dev& d, int np, int64_t r) {
 #ifndef MPC_LAYOUT_GAPS
 #define MPC_LAYOUT_GAPS 256
 #endif
-#ifndef MPC_LOOKBACK_U
-#define MPC_LOOKBACK_U 1
-#endif
 constexpr int kGB = MPC_LAYOUT_GAPS;  // gaps per K_layout block (fewer blocks: a shorter look-back chain)
 
 // K_layout = K_replay + K_assemble in ONE launch: the per-gap replay, then the
@@ -2961,7 +3005,10 @@ __global__ __launch_bounds__(kUB) void K_ins(InsArgs a) {
   for (int64_t gw = (int64_t)w * gridDim.x + blockIdx.x; gw * 64 < a.G; gw += nwaves) {
     const int64_t g = gw * 64 + l;
     if (g >= a.G) continue;
-    const int64_t t0 = (int64_t)a.right_start[g] + g, t1 = (int64_t)a.right_start[g + 1] + g + 1;
+    // this shard's runs of the gap (one GPU: all of them): a shard's LEFT
+    // events fall into the runs its own reads span, [roff, roff + its mixed
+    // RIGHT events of the gap]; K_left wrote nothing into the others
+    const int64_t t0 = (int64_t)a.right_start[g] + g + a.roff[g], t1 = t0 + (a.rsl[g + 1] - a.rsl[g]) + 1;
     const int64_t top = (int64_t)a.row_base[g] + a.lo_f[g] - 1;
     const bool excl = no_ovf && t1 - t0 == 1;
     for (int64_t t = t0; t < t1; ++t) {
@@ -4332,7 +4379,7 @@ int mpc_runs(mpc_plan* p, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   Dev d = p->dev();
   if (p->n_shards > 1) {
-    hipLaunchKernelGGL(K_runs, dim3(1), dim3(1024), 0, st, d);
+    hipLaunchKernelGGL(K_runs, dim3(nblk(p->G + 1, kRunsGB)), dim3(kRunsGB), 0, st, d, next_epoch());
     if (p->N > 0) hipLaunchKernelGGL(K_runR, dim3(std::min<unsigned>(nblk(p->N), 1024)), dim3(256), 0, st, d);
   }
   HIPCHK(hipGetLastError());

@@ -57,12 +57,12 @@ def main():
                "cs_bytes": batch.cs_bytes, "alg_bytes_per_launch": batch.cs_bytes + 24 * batch.n_reads,
                "aligned_bases": batch.aligned_bases, "geometry": plan.info()}
     else:
-        samples, total = bench.shard_samples(pkg, cfg, 0, 1) if bench.CONFIGS[cfg][2] == "strong" else \
-            bench.shard_samples(pkg, cfg, 0, 1)
-        if bench.CONFIGS[cfg][2] == "weak":  # the N x larger global set, split N ways
-            n, reads, _, profile, seed, anti, _ = bench.CONFIGS[cfg]
-            syn = pkg.synth.Synth(n=n, n_reads=reads * W, profile=profile, seed=seed, antisense=anti)
-            samples = [syn.sample(s) for s in range(2 if anti else 1)]
+        # the whole global read set of an N-GPU run (strong: the config's reads;
+        # weak: N x the per-GPU reads), split into N contiguous shards
+        n, reads, scaling, profile, seed, anti, _ = bench.CONFIGS[cfg]
+        syn = pkg.synth.Synth(n=n, n_reads=reads * (W if scaling == "weak" else 1), profile=profile, seed=seed,
+                              antisense=anti)
+        samples = [syn.sample(s) for s in range(2 if anti else 1)]
         sp = dist.ShardedPileup(dist.split_samples(samples, W), [0] * W)
         sp.step(mdf, gtf)
         torch.cuda.synchronize()

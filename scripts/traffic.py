@@ -2,7 +2,10 @@
 """HBM bytes per launch of one kernel from rocprofv3 --pmc passes (FETCH_SIZE and
 WRITE_SIZE in separate passes, scripts/pmc_parse.sh) -> profiles/pmc_traffic.json.
 
-  python3 scripts/traffic.py <pmc-dir> [kernel-substring] [config] [out.json]
+  python3 scripts/traffic.py <pmc-dir> [kernel-substring] [config] [out.json] [n_gpus]
+
+n_gpus > 1: the pass ran scripts/shard_probe.py --mode parse, one rank's shard
+of the n_gpus-shard plan on one GPU (the per-rank K_parse of an N-GPU run).
 
 FETCH_SIZE / WRITE_SIZE are reported in KiB.  Per MI355X_MICROARCH.md (HBM):
 on gfx950 FETCH_SIZE counts exactly half the bytes of 16 B/lane streaming
@@ -14,6 +17,7 @@ d = sys.argv[1]
 pat = sys.argv[2] if len(sys.argv) > 2 else "K_parse"
 cfg = sys.argv[3] if len(sys.argv) > 3 else "c2"
 out = sys.argv[4] if len(sys.argv) > 4 else os.path.join(os.path.dirname(__file__), "..", "profiles", "pmc_traffic.json")
+n_gpus = int(sys.argv[5]) if len(sys.argv) > 5 else 1
 vals = collections.defaultdict(dict)
 for f in glob.glob(d + "/**/*counter_collection.csv", recursive=True):
     for r in csv.DictReader(open(f)):
@@ -31,5 +35,9 @@ rec = {"config": cfg, "kernel": pat, "hbm_bytes_per_launch": fetch + write,
        "dispatches": {k: len(v) for k, v in vals.items()},
        "method": "rocprofv3 --kernel-trace --pmc FETCH_SIZE / WRITE_SIZE in separate passes; FETCH_SIZE x2 "
                  "(gfx950 16 B/lane streaming-read correction), KiB -> bytes"}
+if n_gpus > 1:
+    rec["n_gpus"] = n_gpus
+    rec["method"] += ("; one rank's shard of the %d-shard plan (rank 0, scripts/shard_probe.py --mode parse) on one "
+                      "GPU: the K_parse launch every rank of a %d-GPU run makes" % (n_gpus, n_gpus))
 json.dump(rec, open(out, "w"), indent=1)
 print(json.dumps(rec))

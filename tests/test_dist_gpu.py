@@ -235,3 +235,8 @@ def test_bench_self_launch_two_ranks(tmp_path):
     assert rec["config"]["process_group"] == "gloo"
     assert rec["config"]["global_reads_per_sample"] == 200_000  # weak scaling: 2 x 100k
     assert rec["value"] > 0
+    # the N=2 line carries the per-rank K_parse HBM traffic
+    # rocprofv3 measured on a rank's shard of the 2-shard plan
+    assert rec["roofline"]["traffic"] is not None and rec["roofline"]["traffic"] > 0
+    assert rec["roofline"]["traffic_record"] == "profiles/pmc_traffic_c2_w2.json"
+    assert rec["config"]["batches_in_flight"] == 2  # (--inflight 2 here; the N > 1 default is 2 as well)

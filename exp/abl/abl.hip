@@ -53,7 +53,7 @@
 #endif
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
-    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE)
+    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -375,19 +375,6 @@ template <int WIN> constexpr bool parse_dma() { return MPC_PARSE_DMA && WIN >= 1
 #define MPC_FAST_DECODE_MODES 0x1f
 #endif
 template <int TM> constexpr bool fast_decode() { return (MPC_FAST_DECODE_MODES >> TM) & 1; }
-// Tally mode 3 with ONE substitution window (references up to 16384 bases:
-// C3, C4): the K_parse<3, WIN, NK, true> instantiation takes the round's
-// substitution slots from a wave-uniform count -- no loop over windows, no
-// count kept in a VGPR lane (C3 -1.3 to -1.9 %, C4 -2.2 %); plans with more
-// windows (C5) keep the loop, in a kernel that compiles nothing else
-#ifndef MPC_SUB1
-#define MPC_SUB1 1
-#endif
-// ... and the returning add that takes an insertion event's page slot is
-// issued before the round's other effects (their issue hides its latency)
-#ifndef MPC_EARLY_PLACE
-#define MPC_EARLY_PLACE 0
-#endif
 // ... and tally modes whose rounds find a unit's read base by an LDS round trip
 // (slot base written by the read's start lane, read back by every lane) instead
 // of a scalar pass over the round's read starts: short reads (C1 / C2) start
@@ -730,17 +717,16 @@ __device__ __forceinline__ void chunk_store(uint8_t* p, U8x32 v) {
 // (slot > 64, their adds are discarded by the publish) wait for the new page
 // and try again.  W lives in LDS (tally modes 0-3) or HBM (mode 4).  Every
 // wave reaches the loop's end: an opener never waits.
-// EARLY: the returning add was issued by the caller (`old`), ahead of the
-// round's other effects, so its LDS latency overlaps them.
-template <bool GLOBAL_W, bool EARLY = false>
+template <bool GLOBAL_W>
 __device__ __forceinline__ void parse_place_event(const ParseArgs& a, bool has, uint32_t* W, uint32_t* npg,
-                                                  int64_t pbase, uint32_t* pg0, uint32_t pcap, int b, uint32_t word,
-                                                  uint32_t old = 0u) {
+                                                  int64_t pbase, uint32_t* pg0, uint32_t pcap, int b, uint32_t word) {
   // common case straight-line: the add gives a slot of the current page
   // (pg0 = the workgroup's first page: 32-bit offsets from a scalar base)
-  if constexpr (!EARLY) old = has ? atomicAdd(W, 1u) : 0u;
+  uint32_t old = has ? atomicAdd(W, 1u) : 0u;
   const bool fast = has && (old & ((1u << kPgBits) - 1u)) < (uint32_t)kPgEv;
+#ifndef MPC_ABL_NOEVSTORE
   if (fast) pg0[(old >> kPgBits) * kPgEv + (old & ((1u << kPgBits) - 1u))] = word;
+#endif
   bool need = has && !fast;
   if (!ballot(need)) return;
   // the page is full: open the next one, or wait for its opener.  A waiting
@@ -912,10 +898,8 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, uint3
 // taken by the workgroups that hold such a read; without NK nothing of it is
 // compiled in (its registers would bound every plan's kernel), and a negative
 // tstart is MPC_DE_UNSUPPORTED (parsed from 0, never an out-of-range write).
-// S1: tally mode 3 with one substitution window (MPC_SUB1 above).
-template <int TM, int WIN, bool NK, bool S1 = false>
+template <int TM, int WIN, bool NK>
 __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
-  static_assert(!S1 || TM == 3, "one substitution window: tally mode 3 only");
   constexpr int CH = WIN / 64;
   static_assert(WIN <= kMaxWin, "coordinate bound (kMaxWin)");
   using WL = WaveLds<WIN, lds_base<TM>()>;
@@ -1029,7 +1013,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   int64_t P = readlane64(cbo[chk], 0);
   const int64_t sev_base = (P - a.cs_base) / 3 + 2 * ra;  // ... and its substitution-event regions (TM 3)
   uint32_t nsub_v = 0;                                    // lane k: substitution events of window k
-  uint32_t nsub_s = 0;                                    // ... of the only window (S1, wave-uniform)
   int64_t rs0 = ra;         // first read whose cs starts at or after P
   bool carry = false;       // slot 0 holds a read continuing into this window
   int32_t c_base = 0;       // ... and its coordinate base (wave-uniform): i = base + window prefix of advances
@@ -1440,24 +1423,27 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const int rl = q_read;
       if (NEG && wo_ins && te == 0) te |= push_wo(a, gb + i + n, rl, kWoIns, olen_e, A + sx + 1);
       const bool ok = te == 0 && !wo_ins;
-      const bool ins_inline = ((kind == 3 && olen_e <= kInsInline) || wrap) && ok;
-      const bool any_ins = ballot(ins_inline) != 0;  // (wave-uniform)
-      uint32_t pold = 0u;
-      if (MPC_EARLY_PLACE && any_ins && ins_inline) pold = atomicAdd(bkw + gi / kBW, 1u);  // slot in its bucket's page
+#ifndef MPC_ABL_NOSUB
       if (ok & (kind == 2) & !wrap & (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
+#endif
       const bool del = NEG ? ok & (kind == 4) & (di < n) & (i + olen_e > di) : ok & (kind == 4) & (i >= 0) & (i < n);
+#ifdef MPC_ABL_NODEL
+      if (false) {
+#else
       if (del) {
+#endif
         depth_dec(di);
         depth_inc(i + olen_e < n ? i + olen_e : n);
       }
+#ifndef MPC_ABL_NOLEFT
       if (ok & ((kind == 3) | wrap)) left_bit(gi);
+#endif
       if (ok & (kind == 3) & (olen_e > kInsInline)) push_ovf(a, A + sx + 1, rl, i, olen_e);
-      if (S1) {  // one substitution window: a wave-uniform count
-        const bool sev = ok && kind == 2 && !wrap;
-        const uint64_t bw = ballot(sev);
-        if (sev) a.subev[sev_base + nsub_s + lanes_below(bw)] = (uint16_t)(((uint32_t)i << 2) | pay);
-        nsub_s += (uint32_t)__popcll(bw);
-      } else if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window
+#ifdef MPC_ABL_NOSUB
+      if (false) {
+#else
+      if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window
+#endif
         const bool sev = ok && kind == 2 && !wrap;
         const int win = i >> kSubWinBits;
         uint16_t* wp = a.subev + sev_base;  // window ww's region of this wave
@@ -1466,13 +1452,20 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
           const uint64_t bw = ballot(mine);
           if (!bw) continue;
           const uint32_t n0 = (uint32_t)__builtin_amdgcn_readlane((int)nsub_v, ww);
+#ifndef MPC_ABL_NOSUBSTORE
           if (mine) wp[n0 + lanes_below(bw)] = (uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay);
+#endif
           if (l == ww) nsub_v += (uint32_t)__popcll(bw);
         }
       }
-      if (any_ins)  // the event into its bucket's page (written once)
-        parse_place_event<big, MPC_EARLY_PLACE != 0>(a, ins_inline, bkw + gi / kBW, npg, pbase, pg0, pcap, gi / kBW,
-                                                     ins_word(gi, li, pay, rl - (int)r0), pold);
+      const bool ins_inline = ((kind == 3 && olen_e <= kInsInline) || wrap) && ok;
+#ifdef MPC_ABL_NOPLACE
+      if (false)
+#else
+      if (ballot(ins_inline))  // the event into its bucket's page (written once)
+#endif
+        parse_place_event<big>(a, ins_inline, bkw + gi / kBW, npg, pbase, pg0, pcap, gi / kBW,
+                               ins_word(gi, li, pay, rl - (int)r0));
       if (last) {  // the read's last operation: i_end, downstream check, span
         const int ia = i + adv;
         const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
@@ -1488,7 +1481,9 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         W.s_iend[q] = iw | dnf;
         const int ts = NEG && q_ts < 0 ? 0 : q_ts;  // matches below 0 write nothing
         const int e2 = ie > n ? n : ie;
+#ifndef MPC_ABL_NOSPAN
         if (ts < e2) { depth_inc(ts); depth_dec(e2); }
+#endif
       }
       if (te) flag_read(a, te, rl);
       G += atot;
@@ -1525,8 +1520,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     flag_read(a, DE_OP, r);
     a.i_end[r] = ts < 0 ? 0 : (ts > n ? n + 1 : ts);
   }
-  if (TM == 3 && l < a.sub_wins)
-    a.subev_cnt[((int64_t)blockIdx.x * kMaxCh + chk) * kMaxSubWins + l] = S1 ? nsub_s : nsub_v;
+  if (TM == 3 && l < a.sub_wins) a.subev_cnt[((int64_t)blockIdx.x * kMaxCh + chk) * kMaxSubWins + l] = nsub_v;
   }  // chunks
   };
   if constexpr (NK) {
@@ -3733,11 +3727,9 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
 
 // instantiated (tally mode, window) pairs; packed modes only with 1 and 2 KiB windows
 template <bool NK>
-static const void* parse_kernel_t(int tm, int win, bool s1) {
+static const void* parse_kernel_t(int tm, int win) {
   if (tm == 4) return (const void*)K_parse<4, 1024, NK>;
   if (tm == 2) return win == 1024 ? (const void*)K_parse<2, 1024, NK> : (const void*)K_parse<2, 2048, NK>;
-  if (tm == 3 && s1)
-    return win == 1024 ? (const void*)K_parse<3, 1024, NK, true> : (const void*)K_parse<3, 2048, NK, true>;
   if (tm == 3) return win == 1024 ? (const void*)K_parse<3, 1024, NK> : (const void*)K_parse<3, 2048, NK>;
   if (win == 512) return tm ? (const void*)K_parse<1, 512, NK> : (const void*)K_parse<0, 512, NK>;
   if (win == 2048) return tm ? (const void*)K_parse<1, 2048, NK> : (const void*)K_parse<0, 2048, NK>;
@@ -3745,9 +3737,8 @@ static const void* parse_kernel_t(int tm, int win, bool s1) {
 }
 // the plan's K_parse: with the negative-start rounds only when it holds such reads
 static const void* parse_kernel(const mpc_plan* p) {
-  const bool s1 = MPC_SUB1 && p->tally_mode == 3 && p->sub_wins == 1;
-  return p->in.neg_reads > 0 ? parse_kernel_t<true>(p->tally_mode, p->parse_win, s1)
-                             : parse_kernel_t<false>(p->tally_mode, p->parse_win, s1);
+  return p->in.neg_reads > 0 ? parse_kernel_t<true>(p->tally_mode, p->parse_win)
+                             : parse_kernel_t<false>(p->tally_mode, p->parse_win);
 }
 static void launch_subs(const mpc_plan* p, const Dev& d, hipStream_t st) {
   if (p->work_sub.empty()) return;

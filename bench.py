@@ -305,8 +305,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=None,
                     help="GPUs (one rank each); without a launcher, N > 1 starts N ranks itself "
                          "(torch.distributed.run); under one it must equal WORLD_SIZE")
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=5)
+    # 200 steps: with R batches in flight the timed region starts with the
+    # pipelines empty and ends draining them; at 20 steps that fill / drain was
+    # ~9 % of C2's wall (175 vs 159 us per step, profiles/r06_experiments/
+    # c2_parse_cus_steps.txt) -- a sequencing run streams far more batches
+    ap.add_argument("--steps", type=int, default=200)
+    ap.add_argument("--warmup", type=int, default=10)
     ap.add_argument("--config", default="c2", choices=sorted(CONFIGS))
     ap.add_argument("--kernel-reps", type=int, default=20)
     ap.add_argument("--inflight", type=int, default=None,

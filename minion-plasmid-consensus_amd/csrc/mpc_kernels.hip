@@ -53,7 +53,7 @@
 #endif
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
-    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE)
+    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_LEFT_SKEW)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -93,6 +93,9 @@ constexpr uint32_t kNullGap = 0x3fffffu;
 // 32-61, the 32-bit value below
 constexpr uint64_t kSelAgg = 1ull << 62, kSelPre = 2ull << 62, kSelTag = 0x3fffffffull << 32;
 // look-back predecessors per lane and step (1: 64 per step)
+#ifndef MPC_LEFT_SKEW
+#define MPC_LEFT_SKEW 0
+#endif
 #ifndef MPC_LOOKBACK_U
 #define MPC_LOOKBACK_U 1
 #endif
@@ -2448,6 +2451,12 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     for (int k = threadIdx.x; k < kBW * kMs; k += blockDim.x) Ml[k] = 0;
     for (int k = threadIdx.x; k < kBW * kTs; k += blockDim.x) Tl[k] = 0;
   }
+#if MPC_LEFT_SKEW > 0
+  // the two blocks a CU holds start their unit chains half a phase apart, so one
+  // block's event loads overlap the other's tally (experiment)
+  if ((blockIdx.x & 1) && nunits > (int64_t)gridDim.x)
+    for (int k = 0; k < MPC_LEFT_SKEW; ++k) __builtin_amdgcn_s_sleep(127);
+#endif
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
     if constexpr (kLean) {
       if (threadIdx.x == 0) s_kn = 0;  // ordered before its atomics by load_unit's barriers

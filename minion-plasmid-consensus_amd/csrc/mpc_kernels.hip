@@ -53,7 +53,7 @@
 #endif
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
-    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_LEFT_SKEW)
+    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -93,9 +93,6 @@ constexpr uint32_t kNullGap = 0x3fffffu;
 // 32-61, the 32-bit value below
 constexpr uint64_t kSelAgg = 1ull << 62, kSelPre = 2ull << 62, kSelTag = 0x3fffffffull << 32;
 // look-back predecessors per lane and step (1: 64 per step)
-#ifndef MPC_LEFT_SKEW
-#define MPC_LEFT_SKEW 0
-#endif
 #ifndef MPC_LOOKBACK_U
 #define MPC_LOOKBACK_U 1
 #endif
@@ -2451,12 +2448,6 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
     for (int k = threadIdx.x; k < kBW * kMs; k += blockDim.x) Ml[k] = 0;
     for (int k = threadIdx.x; k < kBW * kTs; k += blockDim.x) Tl[k] = 0;
   }
-#if MPC_LEFT_SKEW > 0
-  // the two blocks a CU holds start their unit chains half a phase apart, so one
-  // block's event loads overlap the other's tally (experiment)
-  if ((blockIdx.x & 1) && nunits > (int64_t)gridDim.x)
-    for (int k = 0; k < MPC_LEFT_SKEW; ++k) __builtin_amdgcn_s_sleep(127);
-#endif
   for (int64_t u = blockIdx.x; u < nunits; u += gridDim.x) {
     if constexpr (kLean) {
       if (threadIdx.x == 0) s_kn = 0;  // ordered before its atomics by load_unit's barriers
@@ -3818,7 +3809,16 @@ static void launch_left(const mpc_plan* p, const Dev& d, hipStream_t st) {
   else hipLaunchKernelGGL(K_left<kUB>, dim3(left_grid(p)), dim3(kUB), 0, st, left_args(p, d));
 }
 static int64_t ins_grid(const mpc_plan* p) { return std::max<int64_t>(1, std::min<int64_t>(p->units_cap, 512)); }
-static int flank_waves(const mpc_plan* p) { return (p->N + kFW * 64 - 1) / (kFW * 64) < 256 ? kFWSmall : kFW; }
+// 2-wave blocks only when 8-wave blocks would leave most CUs idle (C1's 20 k
+// reads: 40 blocks); a C3 shard of 125 k reads (244 blocks of 8 waves) took
+// 47.8 us in 2-wave blocks and 26.6 us in 8-wave ones (threshold 256 -> 128;
+// C1, C2, C3 / 4 shards unchanged: profiles/r06_experiments/k_flank_small_blocks.txt)
+#ifndef MPC_FLANK_SMALL_BELOW
+#define MPC_FLANK_SMALL_BELOW 128
+#endif
+static int flank_waves(const mpc_plan* p) {
+  return (p->N + kFW * 64 - 1) / (kFW * 64) < MPC_FLANK_SMALL_BELOW ? kFWSmall : kFW;
+}
 // K_flank blocks: one per chunk of flank_waves * 64 reads, at most kFlankBlocksMax
 constexpr int64_t kFlankBlocksMax = MPC_FLANK_BLOCKS_MAX;
 static int64_t flank_grid(const mpc_plan* p) {

@@ -2,7 +2,7 @@
 """Time ONE pipeline kernel of library variants (experiments): one full step,
 then the kernel alone re-launched through mpc_profile_kernel (HIP events,
 median of 15).  Re-launches add to stale tallies: timing only.
-  KEXP_CFG=c1..c5 KEXP_KERNEL=parse|left|flank|ins|rsort python3 scripts/kernel_only.py lib1.so [lib2.so ...]"""
+  KEXP_CFG=c1..c5 [KEXP_WORLD=N] KEXP_KERNEL=parse|left|flank|ins|rsort python3 scripts/kernel_only.py lib1.so [lib2.so ...]"""
 import os, subprocess, sys
 
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
@@ -14,7 +14,8 @@ pkg = importlib.import_module("minion-plasmid-consensus_amd")
 eng = pkg.engine
 eng.set_library(os.environ["KEXP_LIB"])  # variant build under test (experiments only)
 import bench
-samples, _ = bench.shard_samples(pkg, os.environ.get("KEXP_CFG", "c2"), 0, 1)
+# KEXP_WORLD=N: rank 0's read slice of an N-GPU run, as one single-GPU batch
+samples, _ = bench.shard_samples(pkg, os.environ.get("KEXP_CFG", "c2"), 0, int(os.environ.get("KEXP_WORLD", "1")))
 which = {"parse": eng.K_PARSE, "left": eng.K_LEFT, "flank": eng.K_FLANK, "ins": eng.K_INS, "rsort": eng.K_RSORT}[os.environ.get("KEXP_KERNEL", "flank")]
 runner = eng.Runner(samples)
 runner.step(0.1, 5.0)

@@ -53,7 +53,8 @@
 #endif
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
-    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW)
+    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW) || \
+    defined(MPC_SPLIT_ROUNDS) || defined(MPC_LEAN_WINDOWS)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -388,6 +389,19 @@ template <int TM> constexpr bool fast_decode() { return (MPC_FAST_DECODE_MODES >
 #ifndef MPC_EARLY_PLACE
 #define MPC_EARLY_PLACE 0
 #endif
+// ... and the rounds of a window run in two loops: canonical rounds (fast
+// decode only) until the first round holding any other unit, then the general
+// decode for the rest of the window (0: one loop, a non-canonical round retried
+// on the general decode in place)
+#ifndef MPC_SPLIT_ROUNDS
+#define MPC_SPLIT_ROUNDS 1
+#endif
+// ... and a window whose units are all canonical -- checked once per window on
+// the lanes' byte masks (chunk_dv) -- runs its rounds without the per-unit
+// check (the lean loop)
+#ifndef MPC_LEAN_WINDOWS
+#define MPC_LEAN_WINDOWS 0
+#endif
 // ... and tally modes whose rounds find a unit's read base by an LDS round trip
 // (slot base written by the read's start lane, read back by every lane) instead
 // of a scalar pass over the round's read starts: short reads (C1 / C2) start
@@ -603,6 +617,31 @@ __device__ __forceinline__ void word_classes(const uint32_t* w, uint32_t* sp, ui
   *sp = s_;
   *cm = c_;
 }
+// Digit and operand-character masks of a lane's staged bytes (lean windows):
+// bit k of dm = byte k is a digit, of vm = a digit or a base (A C G T a c g t),
+// by three v_perm lookups per word: T1[lo & 7] = the high nibbles valid with
+// that low nibble (3: digits, 4-7: the bases), T3[lo >> 1] = every high nibble
+// for lo < 8, only 3 for lo 8-9 (the digits 8, 9), none above; the third
+// lookup is 1 << hi.  Bit 3 of the AND is a digit (hi 3).
+template <int NW>
+__device__ __forceinline__ void word_dv(const uint32_t* w, uint32_t* dm, uint32_t* vm) {
+  uint32_t d_ = 0, v_ = 0;
+#pragma unroll
+  for (int i = 0; i < NW; ++i) {
+    const uint32_t c = w[i];
+    const uint32_t t1 = __builtin_amdgcn_perm(0x580808A8u, 0x58085808u, c & 0x07070707u);
+    const uint32_t t3 = __builtin_amdgcn_perm(0x00000008u, 0xFFFFFFFFu, (c >> 1) & 0x07070707u);
+    const uint32_t t2 = __builtin_amdgcn_perm(0x80402010u, 0x08040201u, (c >> 4) & 0x07070707u);
+    const uint32_t y = t1 & t2 & t3;       // per byte: 0 or one bit (<= 0x80)
+    const uint32_t a7 = ~c & 0x80808080u;  // c < 0x80
+    const uint32_t zv = (y + 0x7F7F7F7Fu) & a7;  // bit 7: y != 0 (no carry out: y <= 0x80)
+    const uint32_t zd = (y << 4) & a7;           // bit 7: y == 8
+    v_ |= hit_nibble(zv) << (4 * i);
+    d_ |= hit_nibble(zd) << (4 * i);
+  }
+  *dm = d_;
+  *vm = v_;
+}
 struct alignas(16) U8x32 { uint4 a, b; };  // a lane's 32 bytes of a 2 KiB window
 __device__ __forceinline__ void chunk_classes(uint2 v, uint32_t* sp, uint32_t* cm) {
   const uint32_t w[2] = {v.x, v.y};
@@ -615,6 +654,18 @@ __device__ __forceinline__ void chunk_classes(uint4 v, uint32_t* sp, uint32_t* c
 __device__ __forceinline__ void chunk_classes(U8x32 v, uint32_t* sp, uint32_t* cm) {
   const uint32_t w[8] = {v.a.x, v.a.y, v.a.z, v.a.w, v.b.x, v.b.y, v.b.z, v.b.w};
   word_classes<8>(w, sp, cm);
+}
+__device__ __forceinline__ void chunk_dv(uint2 v, uint32_t* dm, uint32_t* vm) {
+  const uint32_t w[2] = {v.x, v.y};
+  word_dv<2>(w, dm, vm);
+}
+__device__ __forceinline__ void chunk_dv(uint4 v, uint32_t* dm, uint32_t* vm) {
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  word_dv<4>(w, dm, vm);
+}
+__device__ __forceinline__ void chunk_dv(U8x32 v, uint32_t* dm, uint32_t* vm) {
+  const uint32_t w[8] = {v.a.x, v.a.y, v.a.z, v.a.w, v.b.x, v.b.y, v.b.z, v.b.w};
+  word_dv<8>(w, dm, vm);
 }
 // bits [0, x) set, x in [0, 32]
 __device__ __forceinline__ uint32_t lowmask(int x) { return x >= 32 ? 0xffffffffu : (1u << x) - 1u; }
@@ -1068,6 +1119,8 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     }
     uint32_t spm, cm_own;
     chunk_classes(cur.d, &spm, &cm_own);
+    uint32_t dm_own = 0, vm_own = 0;  // digits / operand characters (lean windows)
+    if constexpr (MPC_LEAN_WINDOWS) chunk_dv(cur.d, &dm_own, &vm_own);
     const uint32_t om_own = spm & ~cm_own;
     put_lane_bits<CH>(W.ra, l, 0u);
     wave_sync_lds();
@@ -1164,6 +1217,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     if (dma && Pn < wend) dma_window<WIN>(a.cs + (Pn & ~(int64_t)15), W.stage[sb ^ 1]);
     // ---- token list: starts in [P, C) (bit 15 = read start), then the sentinel ----
     int T;
+    bool lean = false;  // every unit of the window is canonical (MPC_LEAN_WINDOWS)
     {
       int tlo = (int)(P - cA), thi = (int)(C - cA);
       tlo = tlo < 0 ? 0 : (tlo > CH ? CH : tlo);
@@ -1216,6 +1270,35 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         m &= m - 1;
         W.tok[idx++] = entry(k);
       }
+      if constexpr (MPC_LEAN_WINDOWS) {
+        // Lean window: every unit in [P, C) is canonical, so the rounds take the
+        // fast decode without its per-unit check.  On the lanes' byte masks,
+        // bytes of [P, C) only (P and C are boundaries: no token reaches out):
+        //  * a read starts with a special character (else DE_OP, :100-102)
+        //  * operands have at most 4 bytes (no 5 non-boundary bytes in a row)
+        //  * the operand bytes of a ':' token are digits, of every other token
+        //    bases (A C G T, either case; '-' / 'Z' operands that are not go to
+        //    the checked loop)
+        //  * no empty token is its read's last (:320 applies it)
+        //  * no token runs past the window (far)
+        const uint32_t full = lowmask(CH);
+        const uint32_t N = ~em_own & full;
+        const uint32_t Np = ~from_lane_below(em_own) & full, Cp = from_lane_below(cm_own);
+        auto up = [&](uint32_t own, uint32_t prev, int d) -> uint32_t {  // bit k: bit k - d, the lower lane's below 0
+          if constexpr (CH == 32) return __builtin_amdgcn_alignbit(own, prev, 32u - (uint32_t)d);
+          else return ((own << d) | (prev >> (CH - d))) & full;
+        };
+        const uint32_t b1 = up(N, Np, 1), b2 = up(N, Np, 2), b3 = up(N, Np, 3);
+        const uint32_t r5 = N & b1 & b2 & b3 & up(N, Np, 4);
+        const uint32_t cctx = N & (up(cm_own, Cp, 1) | (up(cm_own, Cp, 2) & b1) | (up(cm_own, Cp, 3) & b1 & b2) |
+                                   (up(cm_own, Cp, 4) & b1 & b2 & b3));  // ':' operand bytes
+        const uint32_t ra_nx = from_lane_above(ra_own);
+        const uint32_t elast = em_own & at(em_own, em_nx, 1) & at(ra_own, ra_nx, 1);  // empty, a read starts after it
+        uint32_t bad = ((ra_own & ~spm) | r5 | (cctx & ~dm_own) | (N & ~cctx & (dm_own | ~vm_own)) | elast) & rng;
+        const int64_t kc = C - 1 - cA;  // the token ending at C: empty and its read's last
+        if (c_rs && kc >= 0 && kc < CH && ((em_own >> kc) & 1u)) bad |= 1u;
+        lean = !far && !ballot(bad != 0);
+      }
       if (l == 0) W.tok[T] = far ? (uint16_t)(kFar | (c_rs ? 0x8000u : 0u)) : (uint16_t)((C - A) | (c_rs ? 0x8000u : 0u));
     }
     wave_sync_lds();
@@ -1226,7 +1309,12 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     int32_t G = 0;  // advances of the window's earlier rounds
     int qc = 0;     // read starts of the window's earlier rounds
     int32_t cb = c_base;  // coordinate base of the open read (wave-uniform)
-    for (int t0 = 0; t0 < T; t0 += 64) {
+    // one round (64 units, one per lane), MODE 2: the general decode; 1: the
+    // fast decode, false (nothing applied) when a unit is not canonical; 0: the
+    // fast decode unchecked (lean window: every unit is canonical)
+    auto round = [&](const int t0, auto modec) -> bool {
+      constexpr int MODE = decltype(modec)::value;
+      constexpr bool GEN = MODE == 2;
       const int t = t0 + l;
       const bool v = t < T;
       const uint32_t t0r = W.tok[t], t1r = W.tok[t + 1];  // in bounds for every lane (+64 padding)
@@ -1257,7 +1345,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       int adv0, adv, kind, olen_e;
       uint32_t pay, err = 0u;
       bool fast = false;
-      if constexpr (fast_decode<TM>()) {
+      if constexpr (!GEN) {
         const uint32_t sh = (uint32_t)(sx & 3);
         uint32_t m0 = b32[sx >> 2], m1 = b32[(sx >> 2) + 1];  // bytes sx .. sx + 4 (sh + 4 <= 7)
         const int pa = (s0 + 1) >> 2;
@@ -1307,8 +1395,19 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         const uint32_t ms = 0u - (uint32_t)star;
         pay = (ms & ((codes >> shl) & 3u)) | (~ms & pk);
         olen_e = ol4;
+        if constexpr (MODE == 0) {
+          // canonical by the window check; what the check lets through beyond
+          // the per-unit one: a 'Z' with an operand and an empty op after a
+          // ':' prefix apply nothing but the prefix (as the general decode)
+          const int act = -(int)((olen > 0) & (op != 'Z'));
+          kind &= act;
+          adv &= act;
+          (void)fast;
+        } else {
+          if (ballot(!fast)) return false;  // (before any effect: the round restarts on the general decode)
+        }
       }
-      if (!fast_decode<TM>() || ballot(!fast)) {  // general decode of the whole round
+      if constexpr (GEN) {  // general decode of the whole round
         const int a4 = sx >> 2;
         const uint32_t sh = (uint32_t)(sx & 3);
         const uint32_t d0 = b32[a4], d1 = b32[a4 + 1], d2 = b32[a4 + 2];
@@ -1444,7 +1543,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const bool any_ins = ballot(ins_inline) != 0;  // (wave-uniform)
       uint32_t pold = 0u;
       if (MPC_EARLY_PLACE && any_ins && ins_inline) pold = atomicAdd(bkw + gi / kBW, 1u);  // slot in its bucket's page
-      if (ok & (kind == 2) & !wrap & (TM != 3 || a.sub_wins == 0)) odd_sub(i, (int)pay);
+      if (ok & (kind == 2) & !wrap & (TM != 3 || (!S1 && a.sub_wins == 0))) odd_sub(i, (int)pay);  // (S1: one window)
       const bool del = NEG ? ok & (kind == 4) & (di < n) & (i + olen_e > di) : ok & (kind == 4) & (i >= 0) & (i < n);
       if (del) {
         depth_dec(di);
@@ -1494,6 +1593,30 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       G += atot;
       qc += __popcll(brs);
       MPC_SEG(4);
+      return true;
+    };
+    int t0 = 0;
+    using Lean = std::integral_constant<int, 0>;
+    using Fast = std::integral_constant<int, 1>;
+    using Gen = std::integral_constant<int, 2>;
+    if (MPC_LEAN_WINDOWS && fast_decode<TM>() && lean) {
+      for (; t0 < T; t0 += 64) round(t0, Lean{});
+    } else if (MPC_LEAN_WINDOWS == 2) {  // (the other windows: the general decode only)
+      for (; t0 < T; t0 += 64) round(t0, Gen{});
+    } else {
+#if MPC_SPLIT_ROUNDS
+    // canonical rounds in one loop; the first round holding any other unit and
+    // the rest of the window take the general decode in a loop of their own,
+    // so its code stays out of the common loop (K_parse -8 to -13 % against
+    // one loop holding both: profiles/r06_experiments/kparse_split_rounds.txt)
+    if constexpr (fast_decode<TM>())
+      for (; t0 < T; t0 += 64)
+        if (!round(t0, Fast{})) break;
+    for (; t0 < T; t0 += 64) round(t0, Gen{});
+#else
+    for (; t0 < T; t0 += 64)
+      if (!fast_decode<TM>() || !round(t0, Fast{})) round(t0, Gen{});
+#endif
     }
     wave_sync_lds();
     // ---- reads that ended in this window: i_end; carry the open one ----

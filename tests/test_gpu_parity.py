@@ -299,6 +299,63 @@ def test_dense_tokens_match_oracle(pkg, seed):
         _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("dense", seed, mdf))
 
 
+def _mixed_cs(rng, n, ts, p_odd):
+    """Valid cs of canonical units (':'-digits + '*' / '+' / '-' with 1-4 byte
+    operands) with, at rate p_odd per unit, a valid token the fast decode does
+    not take: a ':' of 5-6 digits (leading zeros), a 5-7 base insertion, a
+    deletion of non-base bytes, a '*' whose first byte is not a base, a 'Z'
+    with an operand, an empty op right after a ':' prefix, ':0'.  Windows of
+    K_parse then hold canonical units only (the lean loop) or some others
+    (the checked loop and the general decode)."""
+    out, i = ["Z::"], ts
+    stop = int(rng.integers(n // 2, n - 60))
+    while i < stop:
+        out.append(":%d" % int(rng.integers(1, 30)))
+        i += int(out[-1][1:])
+        if rng.random() < p_odd:
+            k = int(rng.integers(0, 7))
+            if k == 0:
+                out.append(":%05d" % int(rng.integers(0, 9))); i += int(out[-1][1:])
+            elif k == 1:
+                out.append("+" + "".join(rng.choice(list("acgtACGT"), int(rng.integers(5, 8)))))
+            elif k == 2:
+                out.append("-" + "".join(rng.choice(list("nNxq"), int(rng.integers(1, 4))))); i += len(out[-1]) - 1
+            elif k == 3:
+                out.append("*n" + str(rng.choice(list("acgt")))); i += 1
+            elif k == 4:
+                out.append("Z" + "".join(rng.choice(list("acgt"), int(rng.integers(1, 4)))))
+            elif k == 5:
+                out.append("*")  # empty: nothing, the ':' before it still advances
+            else:
+                out.append(":0")
+        else:
+            r = rng.random()
+            if r < 0.5:
+                out.append("*" + str(rng.choice(list("acgt"))) + str(rng.choice(list("acgtACGT")))); i += 1
+            elif r < 0.75:
+                out.append("+" + "".join(rng.choice(list("acgtACGT"), int(rng.integers(1, 5)))))
+            else:
+                k = int(rng.integers(1, 5))
+                out.append("-" + "".join(rng.choice(list("acgt"), k))); i += k
+    out.append(":1")
+    return "".join(out)
+
+
+@pytest.mark.parametrize("n,p_odd", [(4000, 0.0), (4000, 0.002), (4000, 0.02), (12000, 0.0), (12000, 0.02)])
+def test_mixed_canonical_windows_match_oracle(pkg, n, p_odd):
+    """Windows of canonical units only, and windows with a few tokens the fast
+    decode does not take (K_parse's per-window check sends those to the checked
+    rounds and the general decode): bit-exact against the oracle, full pileup
+    and at the pipeline's thresholds."""
+    rng = np.random.default_rng(int(p_odd * 1000) + n)
+    ref = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), n).tobytes()
+    ts = [int(rng.integers(0, 200)) for _ in range(400)]
+    css = [_mixed_cs(rng, n, t, p_odd) for t in ts]
+    smp = _packed(ref, css, ts, 11)
+    for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
+        _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("mixed", n, p_odd, mdf))
+
+
 @pytest.mark.parametrize("n,mode,reads", [(300_000, 0, 40), (400_000, 4, 40), (1_500_000, 4, 16)])
 def test_long_reference(pkg, n, mode, reads):
     """A 300 kb reference (parse state in LDS, tally mode 0), a 400 kb one past

@@ -299,21 +299,22 @@ def test_dense_tokens_match_oracle(pkg, seed):
         _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("dense", seed, mdf))
 
 
-def _mixed_cs(rng, n, ts, p_odd):
+def _mixed_cs(rng, n, ts, p_odd, exotic=False):
     """Valid cs of canonical units (':'-digits + '*' / '+' / '-' with 1-4 byte
-    operands) with, at rate p_odd per unit, a valid token the fast decode does
-    not take: a ':' of 5-6 digits (leading zeros), a 5-7 base insertion, a
-    deletion of non-base bytes, a '*' whose first byte is not a base, a 'Z'
-    with an operand, an empty op right after a ':' prefix, ':0'.  Windows of
-    K_parse then hold canonical units only (the lean loop) or some others
-    (the checked loop and the general decode)."""
+    operands) with, at rate p_odd per unit, a valid token the per-unit fast
+    decode does not take: a ':' of 5-6 digits (leading zeros), a 5-7 base
+    insertion, a deletion of non-base bytes, a '*' whose first byte is not a
+    base, a 'Z' with an operand, an empty op right after a ':' prefix, ':0'.
+    The speculative K_parse decodes all of these itself; exotic adds units it
+    does not -- a ':' of 9 digits, a '*' with a 5-byte operand -- so the exact
+    pass redoes the parse."""
     out, i = ["Z::"], ts
     stop = int(rng.integers(n // 2, n - 60))
     while i < stop:
         out.append(":%d" % int(rng.integers(1, 30)))
         i += int(out[-1][1:])
         if rng.random() < p_odd:
-            k = int(rng.integers(0, 7))
+            k = int(rng.integers(0, 9 if exotic else 7))
             if k == 0:
                 out.append(":%05d" % int(rng.integers(0, 9))); i += int(out[-1][1:])
             elif k == 1:
@@ -326,8 +327,12 @@ def _mixed_cs(rng, n, ts, p_odd):
                 out.append("Z" + "".join(rng.choice(list("acgt"), int(rng.integers(1, 4)))))
             elif k == 5:
                 out.append("*")  # empty: nothing, the ':' before it still advances
-            else:
+            elif k == 6:
                 out.append(":0")
+            elif k == 7:
+                out.append(":%09d" % int(rng.integers(0, 9))); i += int(out[-1][1:])
+            else:
+                out.append("*" + "".join(rng.choice(list("acgt"), 5))); i += 1
         else:
             r = rng.random()
             if r < 0.5:
@@ -341,19 +346,47 @@ def _mixed_cs(rng, n, ts, p_odd):
     return "".join(out)
 
 
-@pytest.mark.parametrize("n,p_odd", [(4000, 0.0), (4000, 0.002), (4000, 0.02), (12000, 0.0), (12000, 0.02)])
-def test_mixed_canonical_windows_match_oracle(pkg, n, p_odd):
-    """Windows of canonical units only, and windows with a few tokens the fast
-    decode does not take (K_parse's per-window check sends those to the checked
-    rounds and the general decode): bit-exact against the oracle, full pileup
-    and at the pipeline's thresholds."""
-    rng = np.random.default_rng(int(p_odd * 1000) + n)
+@pytest.mark.parametrize("n,p_odd,exotic", [(4000, 0.0, False), (4000, 0.002, False), (4000, 0.02, False),
+                                             (12000, 0.0, False), (12000, 0.02, False), (4000, 0.002, True),
+                                             (12000, 0.02, True)])
+def test_mixed_canonical_windows_match_oracle(pkg, n, p_odd, exotic):
+    """Canonical units only, a few valid tokens the per-unit fast decode does
+    not take (the speculative K_parse decodes them itself), and (exotic) units
+    it does not decode either, so the gated exact pass redoes the parse
+    (MPC_ST_SPEC): bit-exact against the oracle, full pileup and at the
+    pipeline's thresholds."""
+    eng = pkg.engine
+    rng = np.random.default_rng(int(p_odd * 1000) + n + exotic)
     ref = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), n).tobytes()
     ts = [int(rng.integers(0, 200)) for _ in range(400)]
-    css = [_mixed_cs(rng, n, t, p_odd) for t in ts]
+    css = [_mixed_cs(rng, n, t, p_odd, exotic) for t in ts]
     smp = _packed(ref, css, ts, 11)
     for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
-        _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("mixed", n, p_odd, mdf))
+        _cmp(eng.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("mixed", n, p_odd, exotic, mdf))
+    plan = eng.Plan(eng.Batch([smp]))
+    plan.run(0.1, 5.0)
+    if plan.info()["tally_mode"] in (1, 2, 3):  # (the planes with a speculative parse)
+        assert int(plan.status()[eng.MPC_ST_SPEC]) == int(exotic), ("exact pass ran", exotic)
+
+
+def test_two_byte_substitutions_mode3(pkg):
+    """'*' tokens of two bytes ("*a": valid, :96 writes operand[-1]) packed
+    densely in tally mode 3, where substitutions travel as 2-byte events in a
+    per-chunk region sized from the chunk's cs bytes: one event per two bytes
+    must fit (round 5's regions assumed three bytes per '*' and overran)."""
+    rng = np.random.default_rng(96)
+    n = geo.first_length(3) + 500
+    ref = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), n).tobytes()
+    ts = [int(rng.integers(0, 50)) for _ in range(300)]
+    css = []
+    for t in ts:
+        k = int(rng.integers(n // 3, n - t - 2))
+        css.append("Z::" + "".join("*" + str(rng.choice(list("acgtACGT"))) for _ in range(k)) + ":1")
+    smp = _packed(ref, css, ts, 5)
+    plan = pkg.engine.Plan(pkg.engine.Batch([smp]))
+    assert plan.info()["tally_mode"] == 3
+    for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
+        _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("star2", mdf))
 
 
 @pytest.mark.parametrize("n,mode,reads", [(300_000, 0, 40), (400_000, 4, 40), (1_500_000, 4, 16)])

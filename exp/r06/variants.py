@@ -17,43 +17,11 @@ FAST = ("        fast = !v | (!lfar & ((olen >= 1) & (olen <= 4) & dig &\n"
         "                              (colon | minus | (star & (((bad >> shl) & 0xffu) == 0u)) | (plus & ((bad & vm) == 0u))) |\n"
         "                              nop));")
 
+# (the lean / lazy / speculative / split variants of this round patched switches
+# that commit b26663d holds and the product no longer does: build them from
+# that commit's source)
 VARIANTS = {
     "base": [],
-    # (round 6: "nosplit" -- one loop, a non-canonical round retried in place --
-    # became the default; "split" is the two-loop dispatch)
-    "split": [("#define MPC_SPLIT_ROUNDS 0", "#define MPC_SPLIT_ROUNDS 1")],
-    # speculative pass without the long-operand decode (long ':' / '+' fail over)
-    "spnolong": [("          if (ballot(lng & (colon | plus))) {  // rare: the long operand bytewise from the stage",
-                  "          xok = false;\n          if (false) {")],
-    # the exact K_parse alone (no speculative pass)
-    "nospec": [("#define MPC_SPEC_PARSE 1", "#define MPC_SPEC_PARSE 0")],
-    # windows checked once (byte masks), their rounds without the per-unit check
-    "lean": [("#define MPC_LEAN_WINDOWS 0", "#define MPC_LEAN_WINDOWS 1")],
-    # ... the other windows on the general decode only (two loops, not three)
-    "lean2": [("#define MPC_LEAN_WINDOWS 0", "#define MPC_LEAN_WINDOWS 2")],
-    # structure checked per window, characters per round
-    "lean3": [("#define MPC_LEAN_WINDOWS 0", "#define MPC_LEAN_WINDOWS 3")],
-    # timing: the per-unit check computed, no branch on it (a speculation flag
-    # ORed per lane; right results only on canonical input)
-    "nobranch": [("    const int far_c = (int)(C - A < (1 << 30) ? C - A : (1 << 30));  // wave-uniform",
-                  "    const int far_c = (int)(C - A < (1 << 30) ? C - A : (1 << 30));  // wave-uniform\n    uint32_t spec_bad = 0;"),
-                 ("          if (ballot(!fast)) return false;  // (before any effect: the round restarts on the general decode)",
-                  "          spec_bad |= fast ? 0u : 1u;"),
-                 ("    // ---- reads that ended in this window: i_end; carry the open one ----",
-                  "    if (ballot(spec_bad != 0u) && l == 0) atomicOr(&a.status[7], 1u);\n"
-                  "    // ---- reads that ended in this window: i_end; carry the open one ----")],
-    # diagnostics: windows counted in status[6] (all) / status[7] (not lean)
-    "leandiag": [("#define MPC_LEAN_WINDOWS 0", "#define MPC_LEAN_WINDOWS 2"),
-                 ("        lean = !far && !ballot(bad != 0);",
-                  "        lean = !far && !ballot(bad != 0);\n"
-                  "        if (l == 0) { atomicAdd(&a.status[6], 1u); if (!lean) atomicAdd(&a.status[7], 1u); }")],
-    # timing: every window lean (no check; right results only on canonical input)
-    "leanforce": [("#define MPC_LEAN_WINDOWS 0", "#define MPC_LEAN_WINDOWS 2"),
-                  ("        lean = !far && !ballot(bad != 0);", "        lean = !far; (void)bad;")],
-    # no slot reads in the common round (read index from the slot number)
-    "lazy": [("#define MPC_SLOT_LAZY 0", "#define MPC_SLOT_LAZY 1")],
-    "lean2lazy": [("#define MPC_LEAN_WINDOWS 0", "#define MPC_LEAN_WINDOWS 2"),
-                  ("#define MPC_SLOT_LAZY 0", "#define MPC_SLOT_LAZY 1")],
     # counters: which store stream carries C5's write amplification
     "noevstore": [(PG_STORE, "")],
     "nosubstore": [(S1_STORE, ""), (WIN_STORE, "")],
@@ -63,12 +31,11 @@ VARIANTS = {
         (WIN_STORE, "          if (mine) __builtin_nontemporal_store((uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay), "
                     "wp + n0 + lanes_below(bw));"),
     ],
-    # timing upper bound of a window-level canonical check: the per-round
-    # validity predicate and the general-decode branch dropped (right results
-    # only on canonical input, which the synthetic configs are)
+    # timing upper bound of dropping the per-unit canonical check: no check, no
+    # general decode (right results only on canonical input)
     "nocheck": [(FAST, "        fast = true; (void)dig; (void)bad; (void)vm; (void)nop; (void)lfar;"),
-                ("      if (!fast_decode<TM>() || ballot(!fast)) {  // general decode of the whole round",
-                 "      if (!fast_decode<TM>()) {  // general decode of the whole round")],
+                ("        if (ballot(!fast)) return false;  // (before any effect: the round restarts on the general decode)",
+                 "")],
 }
 
 

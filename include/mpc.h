@@ -85,9 +85,7 @@ extern "C" {
                                multi-workgroup path ran, 2 it was planned but fell back to one workgroup */
 #define MPC_ST_WRAP_EVENTS 6 /* strings written into wrapped odd positions (negative starts, see above) */
 #define MPC_ST_WRAP_POS 7    /* internal: odd positions that received them */
-#define MPC_ST_SPEC 8        /* internal: the speculative parse met a unit it does not decode; the exact
-                               parse redid the launch's parse (mpc_parse) */
-#define MPC_ST_WORDS 9
+#define MPC_ST_WORDS 8
 
 /* Per-read inputs, already in HBM.  One sample = one (assembly, PAF) pair, e.g.
  * the sense and antisense consensus jobs of Snakefile:401-423 in one launch.

@@ -53,8 +53,7 @@
 #endif
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
-    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW) || \
-    defined(MPC_SPLIT_ROUNDS) || defined(MPC_LEAN_WINDOWS) || defined(MPC_SLOT_LAZY) || defined(MPC_SPEC_PARSE)
+    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -389,36 +388,6 @@ template <int TM> constexpr bool fast_decode() { return (MPC_FAST_DECODE_MODES >
 #ifndef MPC_EARLY_PLACE
 #define MPC_EARLY_PLACE 0
 #endif
-// ... and the rounds of a window run in two loops: canonical rounds (fast
-// decode only) until the first round holding any other unit, then the general
-// decode for the rest of the window.  0 (default): one loop, a non-canonical
-// round retried on the general decode in place -- equal or faster at C2-C5
-// (profiles/r06_experiments/kparse_split_lean_variants.txt)
-#ifndef MPC_SPLIT_ROUNDS
-#define MPC_SPLIT_ROUNDS 0
-#endif
-// ... and a window whose units are all canonical -- checked once per window on
-// the lanes' byte masks (chunk_dv) -- runs its rounds without the per-unit
-// check (the lean loop).  1: lean, checked and general loops; 2: lean and
-// general loops; 3: the window check covers the token structure only (no
-// digit / base masks), the rounds check the characters their decode already
-// classifies, and a round failing that takes the general decode in place
-#ifndef MPC_LEAN_WINDOWS
-#define MPC_LEAN_WINDOWS 0
-#endif
-// ... and a unit's read index from its slot number (slot q holds read rs0 - 1 +
-// q), the slot's tstart / i_end loaded only by a read's last unit in the
-// tally modes that find read bases by the scalar pass (3, 4: long reads, about
-// one start per round) -- no slot read in the common round
-#ifndef MPC_SLOT_LAZY
-#define MPC_SLOT_LAZY 0
-#endif
-// ... and the parse runs speculatively first: a K_parse without the general
-// decode, then (gated) the exact one only if the speculative pass met a unit it
-// does not decode (launch_parse)
-#ifndef MPC_SPEC_PARSE
-#define MPC_SPEC_PARSE 0
-#endif
 // ... and tally modes whose rounds find a unit's read base by an LDS round trip
 // (slot base written by the read's start lane, read back by every lane) instead
 // of a scalar pass over the round's read starts: short reads (C1 / C2) start
@@ -433,7 +402,6 @@ template <int TM> constexpr bool fast_decode() { return (MPC_FAST_DECODE_MODES >
 #endif
 template <int TM> constexpr bool bperm_base() { return (MPC_BPERM_BASE_MODES >> TM) & 1; }
 template <int TM> constexpr bool lds_base() { return !bperm_base<TM>() && ((MPC_LDS_BASE_MODES >> TM) & 1); }
-template <int TM> constexpr bool slot_lazy() { return MPC_SLOT_LAZY && !bperm_base<TM>() && !lds_base<TM>(); }
 __host__ __device__ constexpr bool lds_base_rt(int tm) {
   return !((MPC_BPERM_BASE_MODES >> tm) & 1) && ((MPC_LDS_BASE_MODES >> tm) & 1);
 }
@@ -468,7 +436,6 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
   // tallied by K_subs (0 windows: global atomics)
   uint16_t* subev; uint32_t* subev_cnt; int64_t subev_cap; int32_t sub_wins;
   WoEv* wo; int64_t wo_cap;  // strings written into wrapped odd positions (negative starts only)
-  int32_t gate;  // 1: the exact pass after a speculative one -- run only if that one set MPC_ST_SPEC
 };
 
 // Substitution events (tally mode 3, references too long for LDS substitution
@@ -642,31 +609,6 @@ __device__ __forceinline__ void word_classes(const uint32_t* w, uint32_t* sp, ui
   *sp = s_;
   *cm = c_;
 }
-// Digit and operand-character masks of a lane's staged bytes (lean windows):
-// bit k of dm = byte k is a digit, of vm = a digit or a base (A C G T a c g t),
-// by three v_perm lookups per word: T1[lo & 7] = the high nibbles valid with
-// that low nibble (3: digits, 4-7: the bases), T3[lo >> 1] = every high nibble
-// for lo < 8, only 3 for lo 8-9 (the digits 8, 9), none above; the third
-// lookup is 1 << hi.  Bit 3 of the AND is a digit (hi 3).
-template <int NW>
-__device__ __forceinline__ void word_dv(const uint32_t* w, uint32_t* dm, uint32_t* vm) {
-  uint32_t d_ = 0, v_ = 0;
-#pragma unroll
-  for (int i = 0; i < NW; ++i) {
-    const uint32_t c = w[i];
-    const uint32_t t1 = __builtin_amdgcn_perm(0x580808A8u, 0x58085808u, c & 0x07070707u);
-    const uint32_t t3 = __builtin_amdgcn_perm(0x00000008u, 0xFFFFFFFFu, (c >> 1) & 0x07070707u);
-    const uint32_t t2 = __builtin_amdgcn_perm(0x80402010u, 0x08040201u, (c >> 4) & 0x07070707u);
-    const uint32_t y = t1 & t2 & t3;       // per byte: 0 or one bit (<= 0x80)
-    const uint32_t a7 = ~c & 0x80808080u;  // c < 0x80
-    const uint32_t zv = (y + 0x7F7F7F7Fu) & a7;  // bit 7: y != 0 (no carry out: y <= 0x80)
-    const uint32_t zd = (y << 4) & a7;           // bit 7: y == 8
-    v_ |= hit_nibble(zv) << (4 * i);
-    d_ |= hit_nibble(zd) << (4 * i);
-  }
-  *dm = d_;
-  *vm = v_;
-}
 struct alignas(16) U8x32 { uint4 a, b; };  // a lane's 32 bytes of a 2 KiB window
 __device__ __forceinline__ void chunk_classes(uint2 v, uint32_t* sp, uint32_t* cm) {
   const uint32_t w[2] = {v.x, v.y};
@@ -679,18 +621,6 @@ __device__ __forceinline__ void chunk_classes(uint4 v, uint32_t* sp, uint32_t* c
 __device__ __forceinline__ void chunk_classes(U8x32 v, uint32_t* sp, uint32_t* cm) {
   const uint32_t w[8] = {v.a.x, v.a.y, v.a.z, v.a.w, v.b.x, v.b.y, v.b.z, v.b.w};
   word_classes<8>(w, sp, cm);
-}
-__device__ __forceinline__ void chunk_dv(uint2 v, uint32_t* dm, uint32_t* vm) {
-  const uint32_t w[2] = {v.x, v.y};
-  word_dv<2>(w, dm, vm);
-}
-__device__ __forceinline__ void chunk_dv(uint4 v, uint32_t* dm, uint32_t* vm) {
-  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
-  word_dv<4>(w, dm, vm);
-}
-__device__ __forceinline__ void chunk_dv(U8x32 v, uint32_t* dm, uint32_t* vm) {
-  const uint32_t w[8] = {v.a.x, v.a.y, v.a.z, v.a.w, v.b.x, v.b.y, v.b.z, v.b.w};
-  word_dv<8>(w, dm, vm);
 }
 // bits [0, x) set, x in [0, 32]
 __device__ __forceinline__ uint32_t lowmask(int x) { return x >= 32 ? 0xffffffffu : (1u << x) - 1u; }
@@ -989,13 +919,9 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, uint3
 // compiled in (its registers would bound every plan's kernel), and a negative
 // tstart is MPC_DE_UNSUPPORTED (parsed from 0, never an out-of-range write).
 // S1: tally mode 3 with one substitution window (MPC_SUB1 above).
-template <int TM, int WIN, bool NK, bool S1 = false, bool SP = false>
+template <int TM, int WIN, bool NK, bool S1 = false>
 __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   static_assert(!S1 || TM == 3, "one substitution window: tally mode 3 only");
-  static_assert(!SP || fast_decode<TM>(), "the speculative parse is the fast decode");
-  // the gated exact pass (launch_parse): only when the speculative one marked
-  // the launch (block-uniform: every workgroup leaves before any LDS or barrier)
-  if (a.gate && __hip_atomic_load(&a.status[MPC_ST_SPEC], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   constexpr int CH = WIN / 64;
   static_assert(WIN <= kMaxWin, "coordinate bound (kMaxWin)");
   using WL = WaveLds<WIN, lds_base<TM>()>;
@@ -1159,44 +1085,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     const int64_t cA = A + CH * l;
     const uint32_t ra_own = get_lane_bits<CH>(W.ra, l);
     const uint32_t em_own = spm | ra_own;  // boundaries: special characters and read starts
-    // Lean window (MPC_LEAN_WINDOWS): every unit in [P, C) is canonical, so the
-    // rounds take the fast decode without its per-unit check.  On the lanes'
-    // byte masks (here for all bytes; [P, C) is applied once C is known -- P
-    // and C are boundaries, so no token reaches outside):
-    //  * a read starts with a special character (else DE_OP, :100-102)
-    //  * operands have at most 4 bytes (no 5 non-boundary bytes in a row)
-    //  * the operand bytes of a ':' token are digits, of every other token
-    //    bases (A C G T, either case; '-' / 'Z' operands that are not go to
-    //    the checked loop)
-    //  * no empty token is its read's last (:320 applies it): below
-    //  * no token runs past the window (far)
-    uint32_t lean_bad = 0;
-    if constexpr (MPC_LEAN_WINDOWS == 3) {
-      // the structure only: read starts are specials, operands <= 4 bytes
-      const uint32_t full = lowmask(CH);
-      const uint32_t N = ~em_own & full;
-      const uint32_t Np = ~from_lane_below(em_own) & full;
-      auto up = [&](uint32_t own, uint32_t prev, int d) -> uint32_t {  // bit k: bit k - d, the lower lane's below 0
-        if constexpr (CH == 32) return __builtin_amdgcn_alignbit(own, prev, 32u - (uint32_t)d);
-        else return ((own << d) | (prev >> (CH - d))) & full;
-      };
-      lean_bad = (ra_own & ~spm) | (N & up(N, Np, 1) & up(N, Np, 2) & up(N, Np, 3) & up(N, Np, 4));
-    } else if constexpr (MPC_LEAN_WINDOWS) {
-      uint32_t dm, vm;
-      chunk_dv(cur.d, &dm, &vm);
-      const uint32_t full = lowmask(CH);
-      const uint32_t N = ~em_own & full;
-      const uint32_t Np = ~from_lane_below(em_own) & full, Cp = from_lane_below(cm_own);
-      auto up = [&](uint32_t own, uint32_t prev, int d) -> uint32_t {  // bit k: bit k - d, the lower lane's below 0
-        if constexpr (CH == 32) return __builtin_amdgcn_alignbit(own, prev, 32u - (uint32_t)d);
-        else return ((own << d) | (prev >> (CH - d))) & full;
-      };
-      const uint32_t b1 = up(N, Np, 1), b2 = up(N, Np, 2), b3 = up(N, Np, 3);
-      const uint32_t r5 = N & b1 & b2 & b3 & up(N, Np, 4);
-      const uint32_t cctx = N & (up(cm_own, Cp, 1) | (up(cm_own, Cp, 2) & b1) | (up(cm_own, Cp, 3) & b1 & b2) |
-                                 (up(cm_own, Cp, 4) & b1 & b2 & b3));  // ':' operand bytes
-      lean_bad = (ra_own & ~spm) | r5 | (cctx & ~dm) | (N & ~cctx & (dm | ~vm));
-    }
     // ---- cut C: E if E is a boundary (a read start), else the last boundary in (P, E) ----
     const bool e_rs = (E == wend) || (E == o63);
     int64_t C;
@@ -1282,7 +1170,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     if (dma && Pn < wend) dma_window<WIN>(a.cs + (Pn & ~(int64_t)15), W.stage[sb ^ 1]);
     // ---- token list: starts in [P, C) (bit 15 = read start), then the sentinel ----
     int T;
-    bool lean = false;  // every unit of the window is canonical (MPC_LEAN_WINDOWS)
     {
       int tlo = (int)(P - cA), thi = (int)(C - cA);
       tlo = tlo < 0 ? 0 : (tlo > CH ? CH : tlo);
@@ -1335,14 +1222,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         m &= m - 1;
         W.tok[idx++] = entry(k);
       }
-      if constexpr (MPC_LEAN_WINDOWS) {  // (the lean-window check, continued)
-        const uint32_t ra_nx = from_lane_above(ra_own);
-        const uint32_t elast = em_own & at(em_own, em_nx, 1) & at(ra_own, ra_nx, 1);  // empty, a read starts after it
-        uint32_t bad = (lean_bad | elast) & rng;
-        const int64_t kc = C - 1 - cA;  // the token ending at C: empty and its read's last
-        if (c_rs && kc >= 0 && kc < CH && ((em_own >> kc) & 1u)) bad |= 1u;
-        lean = !far && !ballot(bad != 0);
-      }
       if (l == 0) W.tok[T] = far ? (uint16_t)(kFar | (c_rs ? 0x8000u : 0u)) : (uint16_t)((C - A) | (c_rs ? 0x8000u : 0u));
     }
     wave_sync_lds();
@@ -1353,13 +1232,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     int32_t G = 0;  // advances of the window's earlier rounds
     int qc = 0;     // read starts of the window's earlier rounds
     int32_t cb = c_base;  // coordinate base of the open read (wave-uniform)
-    bool spec_bad = false;  // SP: a unit the speculative decode does not take
-    // one round (64 units, one per lane), MODE 3: speculative (SP kernels); 2: the general decode; 1: the
-    // fast decode, false (nothing applied) when a unit is not canonical; 0: the
-    // fast decode unchecked (lean window: every unit is canonical)
-    auto round = [&](const int t0, auto modec) -> bool {
-      constexpr int MODE = decltype(modec)::value;
-      constexpr bool GEN = MODE == 2;
+    // one round (64 units, one per lane): GEN = the general decode; without it
+    // the fast decode, and false (nothing applied) when a unit is not canonical
+    auto round = [&](const int t0, auto genc) -> bool {
+      constexpr bool GEN = decltype(genc)::value;
       const int t = t0 + l;
       const bool v = t < T;
       const uint32_t t0r = W.tok[t], t1r = W.tok[t + 1];  // in bounds for every lane (+64 padding)
@@ -1377,13 +1253,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const uint64_t brs = ballot(is_rs);
       const int q = qc + lanes_below(brs) + (is_rs ? 1 : 0);
       // the read's slot (tstart, read, i_end), loaded before the decode
-      int32_t q_ts = 0, q_read, q_iend = 0;
-      if constexpr (MPC_SLOT_LAZY) {
-        q_read = (int32_t)rs0 - 1 + q;  // slot q >= 1: read rs0 + q - 1; slot 0: the read carried in
-        if constexpr (!slot_lazy<TM>()) { q_ts = W.s_ts[q]; q_iend = W.s_iend[q]; }
-      } else {
-        q_ts = W.s_ts[q]; q_read = W.s_read[q]; q_iend = W.s_iend[q];
-      }
+      const int32_t q_ts = W.s_ts[q], q_read = W.s_read[q], q_iend = W.s_iend[q];
       // ---- decode.  Fast path: every unit of the round is canonical -- an
       // optional absorbed ':' prefix of 1-4 digits, then ':' + 1-4 digits, '*' +
       // 1-4 bytes ending in a base, '+' + 1-4 bases or '-' + 1-4 bytes, ending
@@ -1446,65 +1316,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         const uint32_t ms = 0u - (uint32_t)star;
         pay = (ms & ((codes >> shl) & 3u)) | (~ms & pk);
         olen_e = ol4;
-        if constexpr (MODE == 0) {
-          // canonical by the window check; what the check lets through beyond
-          // the per-unit one: a 'Z' with an operand and an empty op after a
-          // ':' prefix apply nothing but the prefix (as the general decode)
-          const int act = -(int)((olen > 0) & (op != 'Z'));
-          kind &= act;
-          adv &= act;
-          (void)fast;
-          if constexpr (MPC_LEAN_WINDOWS == 3) {
-            // the characters: the unit's ':' digits, a '+' operand's bases, a
-            // '*' operand's last base -- else the round takes the general decode
-            const uint32_t dbad = (((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u & cvm;
-            const uint32_t pbad = plus ? (bad & vm) : 0u, sbad = star ? ((bad >> shl) & 0xffu) : 0u;
-            if (ballot(((dbad | pbad | sbad) != 0u) & v)) return false;
-          }
-        } else if constexpr (MODE == 3) {
-          // Speculative (K_parse<..., SP>): no branch on the check.  Beyond the
-          // canonical units it decodes what minimap2 writes besides -- '-' and
-          // '+' of any length (a long '+' takes the long-insertion path, its
-          // bases checked here) and ':' of 5-8 digits -- and the no-ops a 'Z'
-          // with an operand and an empty op after a ':' prefix (the prefix still
-          // advances, as in the general decode).  Any other unit marks the
-          // launch (spec_bad, MPC_ST_SPEC): its effects are garbage but bounded,
-          // and the gated exact pass redoes the whole parse (launch_parse).
-          const bool lng = (olen > 4) & v & !lfar;
-          uint32_t xval = 0u;
-          bool xok = true;
-          if (ballot(lng & (colon | plus))) {  // rare: the long operand bytewise from the stage
-            if (lng & (colon | plus)) {
-              const uint8_t* s8 = W.stage[sb] + sx + 1;
-              for (int k = 0; k < olen; ++k) {
-                const uint32_t c = s8[k];
-                if (colon) {
-                  xok &= ((c - 0x30u) < 10u) & (k < 8);
-                  xval = xval * 10u + (c - 0x30u);
-                } else {
-                  const uint32_t lc2 = c | 0x20u;
-                  xok &= (lc2 == 0x61u) | (lc2 == 0x63u) | (lc2 == 0x67u) | (lc2 == 0x74u);
-                }
-              }
-            }
-          }
-          const bool zed = op == 'Z';
-          const bool okt = olen <= 4 ? dig & (colon | minus | zed | (star & (((bad >> shl) & 0xffu) == 0u)) |
-                                              (plus & ((bad & vm) == 0u)))
-                                     : dig & (((colon | plus) & xok) | minus | zed);
-          const bool ok_unit = !v | (!lfar & (((olen == 0) & !last & ((pl == 0) | dig) &
-                                               (colon | star | plus | minus | zed)) | ((olen > 0) & okt)));
-          spec_bad |= !ok_unit;
-          const int act = -(int)((olen > 0) & !zed);
-          const int vl = (lng & colon) ? (int)(xval < (uint32_t)kAdvCap ? xval : (uint32_t)kAdvCap) : val;
-          const int dl = olen < kAdvCap ? olen : kAdvCap;
-          kind = act & mv & ((mc & (int)(vl > 0)) | (~mc & (o7 - (o7 >> 2))));
-          adv = act & mv & ((mc & vl) | (int)star | (-(int)minus & dl));
-          olen_e = (minus | plus) ? dl : ol4;
-          (void)fast;
-        } else {
-          if (ballot(!fast)) return false;  // (before any effect: the round restarts on the general decode)
-        }
+        if (ballot(!fast)) return false;  // (before any effect: the round restarts on the general decode)
       }
       if constexpr (GEN) {  // general decode of the whole round
         const int a4 = sx >> 2;
@@ -1600,16 +1412,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       } else {
         for (uint64_t m = brs; m; m &= m - 1) {
           const int j = __ffsll((unsigned long long)m) - 1;
-          int32_t tj;
-          if constexpr (slot_lazy<TM>()) {
-            // the slot's tstart: read rs0 + q_j - 1 is lane q_j - 1's of this window's records
-            const int32_t t = __builtin_amdgcn_readlane(cur.ts, __builtin_amdgcn_readlane(q, j) - 1);
-            const int32_t t0c = !NEG && t < 0 ? 0 : t;
-            tj = t0c < MPC_TSTART_MIN ? MPC_TSTART_MIN : (t0c > kICap ? kICap : t0c);
-          } else {
-            tj = __builtin_amdgcn_readlane(q_ts, j);
-          }
-          cb = tj - (G + __builtin_amdgcn_readlane(aex, j));
+          cb = __builtin_amdgcn_readlane(q_ts, j) - (G + __builtin_amdgcn_readlane(aex, j));
           bv = l >= j ? cb : bv;
         }
       }
@@ -1681,7 +1484,6 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         parse_place_event<big, MPC_EARLY_PLACE != 0>(a, ins_inline, bkw + gi / kBW, npg, pbase, pg0, pcap, gi / kBW,
                                                      ins_word(gi, li, pay, rl - (int)r0), pold);
       if (last) {  // the read's last operation: i_end, downstream check, span
-        if constexpr (slot_lazy<TM>()) { q_ts = W.s_ts[q]; q_iend = W.s_iend[q]; }
         const int ia = i + adv;
         const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
         const int dnf = q_iend & (1 << 30);
@@ -1704,34 +1506,11 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       MPC_SEG(4);
       return true;
     };
-    int t0 = 0;
-    using Lean = std::integral_constant<int, 0>;
-    using Fast = std::integral_constant<int, 1>;
-    using Gen = std::integral_constant<int, 2>;
-    using Spec = std::integral_constant<int, 3>;
-    if constexpr (SP) {
-      for (; t0 < T; t0 += 64) round(t0, Spec{});
-      if (ballot(spec_bad) && l == 0) atomicOr(&a.status[MPC_ST_SPEC], 1u);
-    } else if (MPC_LEAN_WINDOWS == 3 && fast_decode<TM>() && lean) {
-      for (; t0 < T; t0 += 64)
-        if (!round(t0, Lean{})) round(t0, Gen{});
-    } else if (MPC_LEAN_WINDOWS && fast_decode<TM>() && lean) {
-      for (; t0 < T; t0 += 64) round(t0, Lean{});
-    } else if (MPC_LEAN_WINDOWS == 2) {  // (the other windows: the general decode only)
-      for (; t0 < T; t0 += 64) round(t0, Gen{});
-    } else {
-#if MPC_SPLIT_ROUNDS
-    // canonical rounds in one loop; the first round holding any other unit and
-    // the rest of the window take the general decode in a loop of their own
-    if constexpr (fast_decode<TM>())
-      for (; t0 < T; t0 += 64)
-        if (!round(t0, Fast{})) break;
-    for (; t0 < T; t0 += 64) round(t0, Gen{});
-#else
-    for (; t0 < T; t0 += 64)
-      if (!fast_decode<TM>() || !round(t0, Fast{})) round(t0, Gen{});
-#endif
-    }
+    // canonical rounds take the fast decode; a round holding any other unit is
+    // redone on the general decode (one loop: measured against a loop per kind
+    // and against per-window canonical checks, profiles/r06_experiments/)
+    for (int t0 = 0; t0 < T; t0 += 64)
+      if (!fast_decode<TM>() || !round(t0, std::false_type{})) round(t0, std::true_type{});
     wave_sync_lds();
     // ---- reads that ended in this window: i_end; carry the open one ----
     if (l <= nst && (l > 0 || carry) && W.s_end[l] <= C) a.i_end[W.s_read[l]] = W.s_iend[l] & ~(1 << 30);
@@ -3965,7 +3744,6 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.subev = at<uint16_t>(p, mpc_plan::B_SUBEV); a.subev_cnt = at<uint32_t>(p, mpc_plan::B_SUBCNT);
   a.subev_cap = p->subev_cap; a.sub_wins = p->tally_mode == 3 ? p->sub_wins : 0;
   a.wo = d.wo; a.wo_cap = d.wo_cap;
-  a.gate = 0;
   return a;
 }
 
@@ -3987,21 +3765,6 @@ static const void* parse_kernel(const mpc_plan* p) {
   return p->in.neg_reads > 0 ? parse_kernel_t<true>(p->tally_mode, p->parse_win, s1)
                              : parse_kernel_t<false>(p->tally_mode, p->parse_win, s1);
 }
-// ... and its speculative pass (K_parse<..., SP>: the fast decode and no
-// general decode compiled in -- the kernel without it holds fewer registers:
-// K_parse<3, 2048> 40 instead of 88 SGPR spills, 111 instead of 120 VGPRs), in
-// tally modes 1-3 with 1 / 2 KiB windows and no negative starts; nullptr: the
-// plan runs the exact K_parse alone
-static const void* parse_spec_kernel(const mpc_plan* p) {
-  if (!MPC_SPEC_PARSE || p->in.neg_reads > 0 || p->tally_mode < 1 || p->tally_mode > 3) return nullptr;
-  const bool w1 = p->parse_win == 1024;
-  if (p->parse_win != 1024 && p->parse_win != 2048) return nullptr;
-  if (p->tally_mode == 1) return w1 ? (const void*)K_parse<1, 1024, false, false, true> : (const void*)K_parse<1, 2048, false, false, true>;
-  if (p->tally_mode == 2) return w1 ? (const void*)K_parse<2, 1024, false, false, true> : (const void*)K_parse<2, 2048, false, false, true>;
-  if (MPC_SUB1 && p->sub_wins == 1)
-    return w1 ? (const void*)K_parse<3, 1024, false, true, true> : (const void*)K_parse<3, 2048, false, true, true>;
-  return w1 ? (const void*)K_parse<3, 1024, false, false, true> : (const void*)K_parse<3, 2048, false, false, true>;
-}
 static void launch_subs(const mpc_plan* p, const Dev& d, hipStream_t st) {
   if (p->work_sub.empty()) return;
   SubsArgs a;
@@ -4022,20 +3785,10 @@ static void launch_subs(const mpc_plan* p, const Dev& d, hipStream_t st) {
                          (const uint32_t*)a.slab, d.n_of, d.gbase, d.sub);
   }
 }
-static void launch_clear_parse_gated(const mpc_plan* p, const Dev& d, hipStream_t st);
-// The parse: the speculative pass where the plan has one, then -- gated on
-// MPC_ST_SPEC, so both launches leave at once when the speculative pass took
-// every unit -- the parse accumulators re-zeroed and the exact K_parse
 static void launch_parse(const mpc_plan* p, const Dev& d, hipStream_t st) {
   ParseArgs a = parse_args(p, d);
   void* args[] = {&a};
-  const dim3 g(p->n_parse_wg), b(p->parse_nw * 64);
-  if (const void* spk = parse_spec_kernel(p)) {
-    (void)hipLaunchKernel(spk, g, b, args, (size_t)p->parse_lds, st);
-    launch_clear_parse_gated(p, d, st);
-    a.gate = 1;
-  }
-  (void)hipLaunchKernel(parse_kernel(p), g, b, args, (size_t)p->parse_lds, st);
+  (void)hipLaunchKernel(parse_kernel(p), dim3(p->n_parse_wg), dim3(p->parse_nw * 64), args, (size_t)p->parse_lds, st);
 }
 
 static LeftArgs left_args(const mpc_plan* p, const Dev& d) {
@@ -4131,10 +3884,8 @@ struct ClearArgs {
   int64_t words[24];
   uint32_t value[24];
   int32_t n;
-  const uint32_t* gate;  // non-null: clear only if *gate is set (the exact parse after a speculative one)
 };
 __global__ __launch_bounds__(256) void K_clear(ClearArgs c) {
-  if (c.gate && __hip_atomic_load(c.gate, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0u) return;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int k = 0; k < c.n; ++k) {
     uint32_t* p = c.ptr[k];
@@ -4148,30 +3899,6 @@ static inline unsigned nblk(int64_t n, int b = 256) {
   if (g < 1) g = 1;
   if (g > 65535 * 16) g = 65535 * 16;
   return (unsigned)g;
-}
-
-// Before the exact parse that redoes a speculative one: every accumulator
-// K_parse adds into, back to K_clear's values (status but MPC_ST_SPEC, the LEFT
-// bitmap, long-insertion count, depth differences, substitution tallies, the
-// HBM bucket words of tally mode 4); everything else K_parse writes whole
-static void launch_clear_parse_gated(const mpc_plan* p, const Dev& d, hipStream_t st) {
-  ClearArgs c{};
-  auto add = [&](void* ptr, int64_t words, uint32_t v) {
-    c.ptr[c.n] = reinterpret_cast<uint32_t*>(ptr); c.words[c.n] = words; c.value[c.n] = v; ++c.n;
-  };
-  add(d.status, MPC_ST_FIRST_READ, 0u);
-  add(d.status + MPC_ST_FIRST_READ, 1, 0xffffffffu);
-  add(d.status + MPC_ST_FIRST_READ + 1, MPC_ST_SPEC - MPC_ST_FIRST_READ - 1, 0u);
-  add(d.hasleft, (int64_t)(p->sz[mpc_plan::B_HASLEFT] / 4), 0u);
-  add(d.ovf_cnt, 1, 0u);
-  add(d.diff, p->G, 0u);
-  add(d.sub, 4 * p->G, 0u);
-  if (p->tally_mode == 4) {
-    add(at<int32_t>(p, mpc_plan::B_BKCUR), (int64_t)p->n_parse_wg * p->nbmax, kPgInit);
-    add(at<int32_t>(p, mpc_plan::B_BKCNT), (int64_t)p->n_parse_wg * p->nbmax, 0u);
-  }
-  c.gate = d.status + MPC_ST_SPEC;
-  hipLaunchKernelGGL(K_clear, dim3(std::min<unsigned>(nblk(4 * p->G, 256), 256)), dim3(256), 0, st, c);
 }
 
 extern "C" {
@@ -4596,8 +4323,6 @@ int mpc_plan_bind(mpc_plan* p, void* ws, size_t bytes) {
                      hipMemcpyHostToDevice));
   HIPCHK(hipFuncSetAttribute(parse_kernel(p), hipFuncAttributeMaxDynamicSharedMemorySize,
                              p->parse_lds));
-  if (const void* spk = parse_spec_kernel(p))
-    HIPCHK(hipFuncSetAttribute(spk, hipFuncAttributeMaxDynamicSharedMemorySize, p->parse_lds));
   p->bound = true;
   p->runt_dirty = true;
   return MPC_OK;

@@ -17,7 +17,7 @@ LIB_PATH = _build.LIBMPC
 
 ABI_VERSION = 8
 MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED, MPC_ST_RSORT_PATH = 0, 1, 2, 3, 5
-MPC_ST_WRAP_EVENTS, MPC_ST_WRAP_POS, MPC_ST_SPEC = 6, 7, 8
+MPC_ST_WRAP_EVENTS, MPC_ST_WRAP_POS = 6, 7
 DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL, DE_UNSUPPORTED = 1, 2, 4, 8, 16, 32, 64
 (BUF_STATUS, BUF_CALLS, BUF_NCALLS, BUF_MAXDEPTH, BUF_ROWS, BUF_ROWMETA, BUF_RIGHT_CNT, BUF_RIGHT_CNT_ALL,
  BUF_HASLEFT, BUF_MAXR, BUF_RUN_M, BUF_RUN_R, BUF_DIFF, BUF_SUB) = range(14)

@@ -305,9 +305,7 @@ def _mixed_cs(rng, n, ts, p_odd, exotic=False):
     decode does not take: a ':' of 5-6 digits (leading zeros), a 5-7 base
     insertion, a deletion of non-base bytes, a '*' whose first byte is not a
     base, a 'Z' with an operand, an empty op right after a ':' prefix, ':0'.
-    The speculative K_parse decodes all of these itself; exotic adds units it
-    does not -- a ':' of 9 digits, a '*' with a 5-byte operand -- so the exact
-    pass redoes the parse."""
+    exotic adds a ':' of 9 digits and a '*' with a 5-byte operand."""
     out, i = ["Z::"], ts
     stop = int(rng.integers(n // 2, n - 60))
     while i < stop:
@@ -350,11 +348,9 @@ def _mixed_cs(rng, n, ts, p_odd, exotic=False):
                                              (12000, 0.0, False), (12000, 0.02, False), (4000, 0.002, True),
                                              (12000, 0.02, True)])
 def test_mixed_canonical_windows_match_oracle(pkg, n, p_odd, exotic):
-    """Canonical units only, a few valid tokens the per-unit fast decode does
-    not take (the speculative K_parse decodes them itself), and (exotic) units
-    it does not decode either, so the gated exact pass redoes the parse
-    (MPC_ST_SPEC): bit-exact against the oracle, full pileup and at the
-    pipeline's thresholds."""
+    """Canonical units only, and rounds holding a few valid tokens the fast
+    decode does not take (they are redone on the general decode): bit-exact
+    against the oracle, full pileup and at the pipeline's thresholds."""
     eng = pkg.engine
     rng = np.random.default_rng(int(p_odd * 1000) + n + exotic)
     ref = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), n).tobytes()
@@ -363,10 +359,6 @@ def test_mixed_canonical_windows_match_oracle(pkg, n, p_odd, exotic):
     smp = _packed(ref, css, ts, 11)
     for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
         _cmp(eng.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("mixed", n, p_odd, exotic, mdf))
-    plan = eng.Plan(eng.Batch([smp]))
-    plan.run(0.1, 5.0)
-    if plan.info()["tally_mode"] in (1, 2, 3):  # (the planes with a speculative parse)
-        assert int(plan.status()[eng.MPC_ST_SPEC]) == int(exotic), ("exact pass ran", exotic)
 
 
 def test_two_byte_substitutions_mode3(pkg):

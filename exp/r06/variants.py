@@ -31,6 +31,22 @@ VARIANTS = {
         (WIN_STORE, "          if (mine) __builtin_nontemporal_store((uint16_t)(((uint32_t)(i & (kSubWin - 1)) << 2) | pay), "
                     "wp + n0 + lanes_below(bw));"),
     ],
+    # the per-unit check as VALU integers and one compare (fewer 64-bit mask ops);
+    # a '*' needs all its operand bytes to be bases (not only the last)
+    "intcheck_all": [("#define MPC_INT_CHECK_MODES 0x00", "#define MPC_INT_CHECK_MODES 0x1f")],
+    "intcheck_old": [(FAST, """        {  // the check as VALU integers and one compare
+          const uint32_t not4 = (uint32_t)(olen - 1) >> 2;  // 0 iff 1 <= olen <= 4
+          const uint32_t dbad = (((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u & cvm;
+          const uint32_t bbad = (star | plus) ? (bad & vm) : 0u;
+          const uint32_t obad = (colon | star | plus | minus) ? 0u : 1u;
+          fast = !v | (!lfar & (((not4 | dbad | bbad | obad) == 0u) | nop));
+          (void)dig;
+        }""")],
+    # the next window's cs bytes loaded before the rounds
+    "prefetch": [("#define MPC_PREFETCH_CS_MODES 0x00", "#define MPC_PREFETCH_CS_MODES 0x1f")],
+    # both, in tally modes 1 and 2 only (short references: C1, C2)
+    "m12opt": [("#define MPC_PREFETCH_CS_MODES 0x00", "#define MPC_PREFETCH_CS_MODES 0x06"),
+               ("#define MPC_INT_CHECK_MODES 0x00", "#define MPC_INT_CHECK_MODES 0x06")],
     # timing upper bound of dropping the per-unit canonical check: no check, no
     # general decode (right results only on canonical input)
     "nocheck": [(FAST, "        fast = true; (void)dig; (void)bad; (void)vm; (void)nop; (void)lfar;"),

@@ -53,7 +53,8 @@
 #endif
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
-    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW)
+    defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW) || \
+    defined(MPC_PREFETCH_CS_MODES) || defined(MPC_INT_CHECK_MODES)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -388,6 +389,19 @@ template <int TM> constexpr bool fast_decode() { return (MPC_FAST_DECODE_MODES >
 #ifndef MPC_EARLY_PLACE
 #define MPC_EARLY_PLACE 0
 #endif
+// ... and tally modes (bit TM) whose next window's cs bytes are loaded before
+// this window's rounds (registers live across them) instead of after
+#ifndef MPC_PREFETCH_CS_MODES
+#define MPC_PREFETCH_CS_MODES 0x00
+#endif
+template <int TM> constexpr bool prefetch_cs() { return (MPC_PREFETCH_CS_MODES >> TM) & 1; }
+// ... and tally modes (bit TM) whose per-unit canonical check is computed as
+// VALU integers with one compare (a '*' then needs all its operand bytes to be
+// bases, not only the last: the others take the general decode)
+#ifndef MPC_INT_CHECK_MODES
+#define MPC_INT_CHECK_MODES 0x00
+#endif
+template <int TM> constexpr bool int_check() { return (MPC_INT_CHECK_MODES >> TM) & 1; }
 // ... and tally modes whose rounds find a unit's read base by an LDS round trip
 // (slot base written by the read's start lane, read back by every lane) instead
 // of a scalar pass over the round's read starts: short reads (C1 / C2) start
@@ -1168,6 +1182,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     // after the rounds: holding them across the rounds costs VGPRs) ----
     const int64_t Pn = C, rsn = rs0 + nst;
     if (dma && Pn < wend) dma_window<WIN>(a.cs + (Pn & ~(int64_t)15), W.stage[sb ^ 1]);
+    // (prefetch_cs: the next window's cs bytes load now, behind the rounds,
+    // into registers that stay live across them; its read records after them)
+    typename Chunk<CH>::T nxt_d{};
+    if (prefetch_cs<TM>() && !dma && Pn < wend) nxt_d = cs_load<CH>(a.cs + (Pn & ~(int64_t)15) + CH * l);
     // ---- token list: starts in [P, C) (bit 15 = read start), then the sentinel ----
     int T;
     {
@@ -1303,9 +1321,18 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
         // (:309: the operator is only applied to a non-empty operand); no prefix
         // can precede it ('Z' / ':' / '*' / '+' / '-' are never absorbed digits)
         const bool nop = (olen == 0) & !last & (pl == 0) & (colon | star | plus | minus | (op == 'Z'));
-        fast = !v | (!lfar & ((olen >= 1) & (olen <= 4) & dig &
-                              (colon | minus | (star & (((bad >> shl) & 0xffu) == 0u)) | (plus & ((bad & vm) == 0u))) |
-                              nop));
+        if constexpr (int_check<TM>()) {  // VALU integers and one compare
+          const uint32_t not4 = (uint32_t)(olen - 1) >> 2;  // 0 iff 1 <= olen <= 4
+          const uint32_t dbad = (((Tx & 0x7F7F7F7Fu) + 0x76767676u) | Tx) & 0x80808080u & cvm;
+          const uint32_t bbad = (star | plus) ? (bad & vm) : 0u;
+          const uint32_t obad = (colon | star | plus | minus) ? 0u : 1u;
+          fast = !v | (!lfar & (((not4 | dbad | bbad | obad) == 0u) | nop));
+          (void)dig;
+        } else {
+          fast = !v | (!lfar & ((olen >= 1) & (olen <= 4) & dig &
+                                (colon | minus | (star & (((bad >> shl) & 0xffu) == 0u)) | (plus & ((bad & vm) == 0u))) |
+                                nop));
+        }
         // branch-free: '*' 0x2A -> 2, '+' 0x2B -> 3, '-' 0x2D -> 4 from op & 7;
         // ':' -> 1 when it matches at least one base (:77); a no-op: 0
         const int mv = -(int)(v & !nop), mc = -(int)colon;
@@ -1532,7 +1559,14 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     P = Pn;
     rs0 = rsn;
     sb ^= dma ? 1 : 0;
-    if (Pn < wend) cur = fetch_window<CH, !dma>(a, Pn, rsn, l);
+    if (Pn < wend) {
+      if (prefetch_cs<TM>() && !dma) {
+        cur = fetch_window<CH, false>(a, Pn, rsn, l);
+        cur.d = nxt_d;
+      } else {
+        cur = fetch_window<CH, !dma>(a, Pn, rsn, l);
+      }
+    }
     MPC_SEG(5);
   }
   // reads starting at the range end have an empty cs

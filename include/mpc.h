@@ -205,6 +205,10 @@ typedef struct {
   int64_t max_reads_per_workgroup;
   int64_t reads_per_workgroup_cap;
   int64_t workspace_bytes;
+  int32_t deferred_placement;      /* 1: K_parse queues insertion events per wave in LDS and places them
+                                      64 at a time (2 KiB windows, tally mode 1 or 3 with one
+                                      substitution window, when the queues fit the LDS budget) */
+  int32_t reserved;
 } mpc_plan_info;
 int mpc_plan_get_info(const mpc_plan* plan, mpc_plan_info* info);
 #define MPC_OVR_GEOMETRY 1 /* MPC_PARSE_GEOMETRY="tm,win,nw" picked the parse geometry */

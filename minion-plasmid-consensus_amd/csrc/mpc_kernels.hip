@@ -54,7 +54,7 @@
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
     defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW) || \
-    defined(MPC_PREFETCH_CS_MODES) || defined(MPC_INT_CHECK_MODES)
+    defined(MPC_PREFETCH_CS_MODES) || defined(MPC_INT_CHECK_MODES) || defined(MPC_DEFER_PLACE)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -402,6 +402,14 @@ template <int TM> constexpr bool prefetch_cs() { return (MPC_PREFETCH_CS_MODES >
 #define MPC_INT_CHECK_MODES 0x00
 #endif
 template <int TM> constexpr bool int_check() { return (MPC_INT_CHECK_MODES >> TM) & 1; }
+// ... and insertion events are queued per wave in LDS (kDefQ entries) and
+// placed 64 at a time, one per lane, instead of in every round that holds one
+// (2 KiB windows, tally modes 1 and 3 with one substitution window, when the
+// queues fit the LDS budget)
+#ifndef MPC_DEFER_PLACE
+#define MPC_DEFER_PLACE 1
+#endif
+constexpr int kDefQ = 128;  // queue entries per wave (a power of 2, >= 127)
 // ... and tally modes whose rounds find a unit's read base by an LDS round trip
 // (slot base written by the read's start lane, read back by every lane) instead
 // of a scalar pass over the round's read starts: short reads (C1 / C2) start
@@ -450,6 +458,7 @@ struct ParseArgs {  // slim argument block (no SGPR spills)
   // tallied by K_subs (0 windows: global atomics)
   uint16_t* subev; uint32_t* subev_cnt; int64_t subev_cap; int32_t sub_wins;
   WoEv* wo; int64_t wo_cap;  // strings written into wrapped odd positions (negative starts only)
+  int32_t defer_off;  // deferred placement (K_parse DP): LDS byte offset of the per-wave event queues
 };
 
 // Substitution events (tally mode 3, references too long for LDS substitution
@@ -933,9 +942,10 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, uint3
 // compiled in (its registers would bound every plan's kernel), and a negative
 // tstart is MPC_DE_UNSUPPORTED (parsed from 0, never an out-of-range write).
 // S1: tally mode 3 with one substitution window (MPC_SUB1 above).
-template <int TM, int WIN, bool NK, bool S1 = false>
+template <int TM, int WIN, bool NK, bool S1 = false, bool DP = false>
 __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   static_assert(!S1 || TM == 3, "one substitution window: tally mode 3 only");
+  static_assert(!DP || TM != 4, "deferred placement: bucket words in LDS");
   constexpr int CH = WIN / 64;
   static_assert(WIN <= kMaxWin, "coordinate bound (kMaxWin)");
   using WL = WaveLds<WIN, lds_base<TM>()>;
@@ -1040,6 +1050,19 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   auto take_chunk = [&]() {
     const uint32_t v = atomicAdd(cnext, l == 0 ? 1u : 0u);
     return uniform_i32(__builtin_amdgcn_readlane((int)v, 0));
+  };
+  // deferred placement: the wave's queue of (bucket, event word) in LDS, a ring
+  // of kDefQ entries between dq_tail and dq_head (wave-uniform counters); a
+  // round appends its events, and 64 at a time are placed after it (<= 63 wait
+  // before a round, <= 127 after one)
+  uint2* const dq = DP ? reinterpret_cast<uint2*>(lds + a.defer_off) + w * kDefQ : nullptr;
+  uint32_t dq_head = 0, dq_tail = 0;
+  auto defer_flush = [&](const int cnt) {  // the cnt (<= 64) oldest events, one per lane
+    wave_sync_lds();
+    const bool has = l < cnt;
+    const uint2 e = has ? dq[(dq_tail + l) & (kDefQ - 1)] : make_uint2(0u, 0u);
+    parse_place_event<big>(a, has, bkw + e.x, npg, pbase, pg0, pcap, (int)e.x, e.y);
+    dq_tail += (uint32_t)cnt;
   };
   auto chunks = [&](auto negc) {
   constexpr bool NEG = decltype(negc)::value;
@@ -1480,7 +1503,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       const bool ins_inline = ((kind == 3 && olen_e <= kInsInline) || wrap) && ok;
       const bool any_ins = ballot(ins_inline) != 0;  // (wave-uniform)
       uint32_t pold = 0u;
-      if (MPC_EARLY_PLACE && any_ins && ins_inline) pold = atomicAdd(bkw + gi / kBW, 1u);  // slot in its bucket's page
+      if (!DP && MPC_EARLY_PLACE && any_ins && ins_inline) pold = atomicAdd(bkw + gi / kBW, 1u);  // slot in its bucket's page
       if (ok & (kind == 2) & !wrap & (TM != 3 || (!S1 && a.sub_wins == 0))) odd_sub(i, (int)pay);  // (S1: one window)
       const bool del = NEG ? ok & (kind == 4) & (di < n) & (i + olen_e > di) : ok & (kind == 4) & (i >= 0) & (i < n);
       if (del) {
@@ -1507,9 +1530,15 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
           if (l == ww) nsub_v += (uint32_t)__popcll(bw);
         }
       }
-      if (any_ins)  // the event into its bucket's page (written once)
+      if (DP) {  // the event into the wave's queue
+        const uint64_t bi = ballot(ins_inline);
+        if (ins_inline)
+          dq[(dq_head + lanes_below(bi)) & (kDefQ - 1)] = make_uint2((uint32_t)(gi / kBW), ins_word(gi, li, pay, rl - (int)r0));
+        dq_head += (uint32_t)__popcll(bi);
+      } else if (any_ins) {  // the event into its bucket's page (written once)
         parse_place_event<big, MPC_EARLY_PLACE != 0>(a, ins_inline, bkw + gi / kBW, npg, pbase, pg0, pcap, gi / kBW,
                                                      ins_word(gi, li, pay, rl - (int)r0), pold);
+      }
       if (last) {  // the read's last operation: i_end, downstream check, span
         const int ia = i + adv;
         const int ie = ia < 0 ? 0 : (ia > n ? n + 1 : ia);
@@ -1536,8 +1565,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     // canonical rounds take the fast decode; a round holding any other unit is
     // redone on the general decode (one loop: measured against a loop per kind
     // and against per-window canonical checks, profiles/r06_experiments/)
-    for (int t0 = 0; t0 < T; t0 += 64)
+    for (int t0 = 0; t0 < T; t0 += 64) {
       if (!fast_decode<TM>() || !round(t0, std::false_type{})) round(t0, std::true_type{});
+      if (DP && dq_head - dq_tail >= 64u) defer_flush(64);
+    }
     wave_sync_lds();
     // ---- reads that ended in this window: i_end; carry the open one ----
     if (l <= nst && (l > 0 || carry) && W.s_end[l] <= C) a.i_end[W.s_read[l]] = W.s_iend[l] & ~(1 << 30);
@@ -1585,6 +1616,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   } else {
     chunks(std::false_type{});
   }
+  if (DP && dq_head != dq_tail) defer_flush((int)(dq_head - dq_tail));  // (<= 63)
   MPC_SEG(5);
   // every LDS-DMA was waited for by the window after it (one is issued only
   // when another window follows); drain anyway before the LDS is reused
@@ -3700,6 +3732,7 @@ struct mpc_plan {
   int32_t sub_wins = 0;                               // tally mode 3: substitution-event windows
   int64_t subev_cap = 0;
   int n_parse_wg = 0, parse_lds = 0, nbmax = 1, parse_win = 1024, parse_nw = 8;
+  int defer_off = 0;                                  // K_parse deferred placement: its queues' LDS offset (0: off)
   int64_t n_bc = 0, units_cap = 0, max_wg_reads = 0;
   int32_t left_ub = 1024;  // K_left threads per block
   int32_t shard = 0, n_shards = 1;
@@ -3778,6 +3811,7 @@ static ParseArgs parse_args(const mpc_plan* p, const Dev& d) {
   a.subev = at<uint16_t>(p, mpc_plan::B_SUBEV); a.subev_cnt = at<uint32_t>(p, mpc_plan::B_SUBCNT);
   a.subev_cap = p->subev_cap; a.sub_wins = p->tally_mode == 3 ? p->sub_wins : 0;
   a.wo = d.wo; a.wo_cap = d.wo_cap;
+  a.defer_off = p->defer_off;
   return a;
 }
 
@@ -3796,6 +3830,9 @@ static const void* parse_kernel_t(int tm, int win, bool s1) {
 // the plan's K_parse: with the negative-start rounds only when it holds such reads
 static const void* parse_kernel(const mpc_plan* p) {
   const bool s1 = MPC_SUB1 && p->tally_mode == 3 && p->sub_wins == 1;
+  if (p->defer_off > 0)  // (planner: 2 KiB windows, tally mode 1 or 3 with s1, no negative starts)
+    return p->tally_mode == 1 ? (const void*)K_parse<1, 2048, false, false, true>
+                              : (const void*)K_parse<3, 2048, false, true, true>;
   return p->in.neg_reads > 0 ? parse_kernel_t<true>(p->tally_mode, p->parse_win, s1)
                              : parse_kernel_t<false>(p->tally_mode, p->parse_win, s1);
 }
@@ -4177,6 +4214,17 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
           p->subsum_rows = std::max(p->subsum_rows, b1 - b0);
         }
     }
+    // deferred placement: the per-wave queues after the parse LDS, when they fit
+    p->defer_off = 0;
+    if (MPC_DEFER_PLACE && p->parse_win == 2048 && p->in.neg_reads == 0 &&
+        (p->tally_mode == 1 || (MPC_SUB1 && p->tally_mode == 3 && p->sub_wins == 1))) {
+      const int off = (p->parse_lds + 15) & ~15;
+      const int end = off + p->parse_nw * kDefQ * (int)sizeof(uint2);
+      if (end <= lds_cap && std::max(1, std::min(lds_cap / end, max_waves_cu / p->parse_nw)) == per_cu) {
+        p->defer_off = off;
+        p->parse_lds = end;
+      }
+    }
     for (int s = 0; s < p->S; ++s) {
       const int nb = (int)((p->ref_len[s] + 1 + kBW - 1) / kBW);
       if (pw_begin[s + 1] == pw_begin[s]) continue;  // no reads: nothing to tally
@@ -4299,6 +4347,8 @@ int mpc_plan_get_info(const mpc_plan* p, mpc_plan_info* info) {
   info->parse_window = p->parse_win;
   info->parse_waves = p->parse_nw;
   info->parse_lds_bytes = p->parse_lds;
+  info->deferred_placement = p->defer_off > 0 ? 1 : 0;
+  info->reserved = 0;
   info->parse_workgroups = p->n_parse_wg;
   info->max_reads_per_workgroup = p->max_wg_reads;
   info->reads_per_workgroup_cap = wg_reads_cap(p->tally_mode);

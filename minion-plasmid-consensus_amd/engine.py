@@ -52,7 +52,7 @@ class PlanInfo(ctypes.Structure):
         ("tally_mode", ctypes.c_int32), ("parse_window", ctypes.c_int32), ("parse_waves", ctypes.c_int32),
         ("parse_lds_bytes", ctypes.c_int32), ("parse_workgroups", ctypes.c_int32), ("overrides", ctypes.c_int32),
         ("max_reads_per_workgroup", ctypes.c_int64), ("reads_per_workgroup_cap", ctypes.c_int64),
-        ("workspace_bytes", ctypes.c_int64),
+        ("workspace_bytes", ctypes.c_int64), ("deferred_placement", ctypes.c_int32), ("reserved", ctypes.c_int32),
     ]
 
     def as_dict(self):
@@ -224,9 +224,10 @@ def set_library(path):
 
 
 def geometry(ref_lens, reads_per_sample, cs_bytes, n_reads_global=None, read_offset=0, shard=0, n_shards=1,
-             parse_cus=0):
+             parse_cus=0, neg_reads=0):
     """Host-only planning (no device): the mpc_plan_info a Plan over inputs of
-    this shape would use (``parse_cus`` as for Batch).  Needs no GPU."""
+    this shape would use (``parse_cus`` as for Batch; ``neg_reads``: reads with
+    a negative tstart).  Needs no GPU."""
     ref_len = np.ascontiguousarray(ref_lens, dtype=np.int64)
     counts = np.asarray(reads_per_sample, dtype=np.int64)
     rb = np.ascontiguousarray(np.concatenate([[0], np.cumsum(counts)]), dtype=np.int64)
@@ -234,7 +235,7 @@ def geometry(ref_lens, reads_per_sample, cs_bytes, n_reads_global=None, read_off
     inp = _Input(n_samples=len(ref_len), h_ref_len=ref_len.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)),
                  h_read_begin=rb.ctypes.data_as(ctypes.POINTER(ctypes.c_int64)), n_reads=n, cs_bytes=int(cs_bytes),
                  cs_base=0, read_offset=read_offset, n_reads_global=n_reads_global or n, shard=shard,
-                 n_shards=n_shards, parse_cus=int(parse_cus))
+                 n_shards=n_shards, parse_cus=int(parse_cus), neg_reads=int(neg_reads))
     L = lib()
     h = ctypes.c_void_p()
     _check(L.mpc_plan_create(ctypes.byref(inp), int((4 * ref_len + 8).sum() + 1024), ctypes.byref(h)))

@@ -74,6 +74,26 @@ def test_planner_geometry(pkg):
         assert info["parse_lds_bytes"] <= 160 * 1024 and info["parse_waves"] in (8, 10, 12, 16)
 
 
+def test_planner_deferred_placement(pkg):
+    """K_parse queues insertion events per wave in LDS (mpc_kernels.hip
+    MPC_DEFER_PLACE) only with 2 KiB windows in tally mode 1 or 3 with one
+    substitution window, and only when the queues fit the LDS budget without
+    changing the geometry: C2-C4 take it, C1 and C5 (LDS full) do not; reads
+    with negative starts keep inline placement (the plan binds that K_parse)."""
+    g = pkg.engine.geometry
+    on = [g([2686, 2686], [100_000, 100_000], 63 << 20), g([10_000], [1_000_000], 1200 << 20),
+          g([10_000] * 2, [100_000] * 2, 1070 << 20)]
+    off = [g([5000], [20_000], 20_000 * 600), g([30_000] * 24, [10_000] * 24, 24 * 3600 * 10_000 // 100)]
+    for info in on:
+        assert info["deferred_placement"] == 1 and info["parse_window"] == 2048
+        assert info["tally_mode"] in (1, 3) and info["parse_lds_bytes"] <= 160 * 1024
+    for info in off:
+        assert info["deferred_placement"] == 0
+    neg = g([2686, 2686], [100_000, 100_000], 63 << 20, neg_reads=1)
+    assert neg["deferred_placement"] == 0
+    assert 0 <= on[0]["parse_lds_bytes"] - 16 * 128 * 8 - neg["parse_lds_bytes"] < 16  # (16-byte aligned queues)
+
+
 def test_planner_parse_cus(pkg):
     """mpc_input.parse_cus (bench.py with batches in flight): the parse grid is
     one balanced wave of resident workgroups on that many CUs -- fewer

@@ -381,6 +381,36 @@ def test_two_byte_substitutions_mode3(pkg):
         _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("star2", mdf))
 
 
+@pytest.mark.parametrize("mode,reads", [(1, 400), (3, 300), (1, 1), (3, 2)])
+def test_deferred_placement_dense_insertions(pkg, mode, reads):
+    """Insertions queued per wave in LDS and placed 64 at a time
+    (mpc_kernels.hip MPC_DEFER_PLACE; mpc_plan_info.deferred_placement): reads
+    of dense 1-4 base '+' tokens (every round fills the queue, bucket pages
+    open during the flushes) plus longer ones (the overflow list, not queued),
+    and single reads whose few events wait in the queue until the last flush."""
+    rng = np.random.default_rng(400 + mode + reads)
+    n = 3000 if mode == 1 else geo.first_length(3) + 500
+    ref = rng.choice(np.frombuffer(b"ACGT", dtype=np.uint8), n).tobytes()
+    css, ts = [], []
+    for r in range(reads):
+        t = int(rng.integers(0, 50))
+        parts, i = ["Z"], t
+        stop = n - 60 if reads > 2 else t + 40
+        while i < stop:
+            m = int(rng.integers(1, 4))
+            parts.append(":%d" % m)
+            i += m
+            k = int(rng.integers(1, 5)) if rng.random() < 0.9 else int(rng.integers(5, 9))
+            parts.append("+" + "".join(rng.choice(list("acgt"), k)))
+        css.append("".join(parts) + ":2")
+        ts.append(t)
+    smp = _packed(ref, css, ts, 7)
+    info = pkg.engine.Plan(pkg.engine.Batch([smp])).info()
+    assert info["tally_mode"] == mode and info["deferred_placement"] == 1, info
+    for mdf, gtf in ((-1.0, 1.0), (0.1, 5.0)):
+        _cmp(pkg.engine.pileup([smp], mdf, gtf)[0], _oracle(smp, mdf, gtf), ("defer", mode, reads, mdf))
+
+
 @pytest.mark.parametrize("n,mode,reads", [(300_000, 0, 40), (400_000, 4, 40), (1_500_000, 4, 16)])
 def test_long_reference(pkg, n, mode, reads):
     """A 300 kb reference (parse state in LDS, tally mode 0), a 400 kb one past

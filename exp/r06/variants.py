@@ -45,7 +45,7 @@ VARIANTS = {
     # the next window's cs bytes loaded before the rounds
     "noflush": [("      if (dv) atomicAdd(a.diff + gb + p, dv);", "      (void)dv;"),
                 ("      if (v) atomicAdd(sg + k, v);", "      (void)v; (void)sg;")],
-    "nodefersub": [("#define MPC_DEFER_SUBEV 1", "#define MPC_DEFER_SUBEV 0")],
+    "defersub": [("#define MPC_DEFER_SUBEV 0", "#define MPC_DEFER_SUBEV 1")],
     "nodefer": [("#define MPC_DEFER_PLACE 1", "#define MPC_DEFER_PLACE 0")],
     "prefetch": [("#define MPC_PREFETCH_CS_MODES 0x00", "#define MPC_PREFETCH_CS_MODES 0x1f")],
     # both, in tally modes 1 and 2 only (short references: C1, C2)

@@ -54,7 +54,7 @@
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
     defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW) || \
-    defined(MPC_PREFETCH_CS_MODES) || defined(MPC_INT_CHECK_MODES) || defined(MPC_DEFER_PLACE)
+    defined(MPC_PREFETCH_CS_MODES) || defined(MPC_INT_CHECK_MODES) || defined(MPC_DEFER_PLACE) || defined(MPC_DEFER_SUBEV)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -410,6 +410,18 @@ template <int TM> constexpr bool int_check() { return (MPC_INT_CHECK_MODES >> TM
 #define MPC_DEFER_PLACE 1
 #endif
 constexpr int kDefQ = 128;  // queue entries per wave (a power of 2, >= 127)
+// ... and (tally mode 3 with one substitution window) the 2-byte substitution
+// events too: a ring of kSubQ per wave, written out 128 at a time (two
+// consecutive events per lane) instead of one global store per round
+// (off: bit-exact, but C3 +7.7 %, C4 +6.5 % -- 120 instead of 89 SGPR spills;
+// profiles/r06_experiments/kparse_deferred_subev.txt)
+#ifndef MPC_DEFER_SUBEV
+#define MPC_DEFER_SUBEV 0
+#endif
+constexpr int kSubQ = 256;  // substitution-event ring per wave (a power of 2, >= 191)
+__host__ __device__ constexpr int defer_bytes(int nw, bool subq) {
+  return nw * (kDefQ * 8 + (subq ? kSubQ * 2 : 0));
+}
 // ... and tally modes whose rounds find a unit's read base by an LDS round trip
 // (slot base written by the read's start lane, read back by every lane) instead
 // of a scalar pass over the round's read starts: short reads (C1 / C2) start
@@ -1057,6 +1069,10 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   // before a round, <= 127 after one)
   uint2* const dq = DP ? reinterpret_cast<uint2*>(lds + a.defer_off) + w * kDefQ : nullptr;
   uint32_t dq_head = 0, dq_tail = 0;
+  // ... and the chunk's substitution events (S1): ring index = event index in
+  // the chunk's region; sq_tail of them are in HBM (nsub_s = the head)
+  constexpr bool DQS = DP && S1 && MPC_DEFER_SUBEV;
+  uint16_t* const sq = DQS ? reinterpret_cast<uint16_t*>(lds + a.defer_off + nw * kDefQ * 8) + w * kSubQ : nullptr;
   auto defer_flush = [&](const int cnt) {  // the cnt (<= 64) oldest events, one per lane
     wave_sync_lds();
     const bool has = l < cnt;
@@ -1073,7 +1089,16 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
   const int64_t sev_base = (P - a.cs_base) / kSubEvBytes + 2 * ra;  // ... and its substitution-event regions (TM 3)
   uint32_t nsub_v = 0;                                    // lane k: substitution events of window k
   uint32_t nsub_s = 0;                                    // ... of the only window (S1, wave-uniform)
-  int64_t rs0 = ra;         // first read whose cs starts at or after P
+  uint32_t sq_tail = 0;                                   // (DQS) ... written to the region
+  auto sub_flush = [&](const uint32_t cnt) {  // the cnt (<= 128) oldest queued events, two per lane
+    wave_sync_lds();
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const uint32_t k = sq_tail + 2u * (uint32_t)l + (uint32_t)h;
+      if (k < sq_tail + cnt) a.subev[sev_base + k] = sq[k & (kSubQ - 1)];
+    }
+    sq_tail += cnt;
+  };  int64_t rs0 = ra;         // first read whose cs starts at or after P
   bool carry = false;       // slot 0 holds a read continuing into this window
   int32_t c_base = 0;       // ... and its coordinate base (wave-uniform): i = base + window prefix of advances
   constexpr bool dma = parse_dma<WIN>();
@@ -1515,7 +1540,12 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
       if (S1) {  // one substitution window: a wave-uniform count
         const bool sev = ok && kind == 2 && !wrap;
         const uint64_t bw = ballot(sev);
-        if (sev) a.subev[sev_base + nsub_s + lanes_below(bw)] = (uint16_t)(((uint32_t)i << 2) | pay);
+        const uint16_t ev = (uint16_t)(((uint32_t)i << 2) | pay);
+        if (DQS) {
+          if (sev) sq[(nsub_s + lanes_below(bw)) & (kSubQ - 1)] = ev;
+        } else {
+          if (sev) a.subev[sev_base + nsub_s + lanes_below(bw)] = ev;
+        }
         nsub_s += (uint32_t)__popcll(bw);
       } else if (TM == 3 && a.sub_wins > 0) {  // substitution events, wave-aggregated per window
         const bool sev = ok && kind == 2 && !wrap;
@@ -1568,6 +1598,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     for (int t0 = 0; t0 < T; t0 += 64) {
       if (!fast_decode<TM>() || !round(t0, std::false_type{})) round(t0, std::true_type{});
       if (DP && dq_head - dq_tail >= 64u) defer_flush(64);
+      if (DQS && nsub_s - sq_tail >= 128u) sub_flush(128u);
     }
     wave_sync_lds();
     // ---- reads that ended in this window: i_end; carry the open one ----
@@ -1606,6 +1637,7 @@ __global__ __launch_bounds__(kMaxPW * 64) void K_parse(ParseArgs a) {
     flag_read(a, DE_OP, r);
     a.i_end[r] = ts < 0 ? 0 : (ts > n ? n + 1 : ts);
   }
+  if (DQS && nsub_s != sq_tail) sub_flush(nsub_s - sq_tail);  // (<= 127)
   if (TM == 3 && l < a.sub_wins)
     a.subev_cnt[((int64_t)blockIdx.x * kMaxCh + chk) * kMaxSubWins + l] = S1 ? nsub_s : nsub_v;
   }  // chunks
@@ -4219,7 +4251,7 @@ int mpc_plan_create(const mpc_input* in, int64_t row_cap, mpc_plan** out) {
     if (MPC_DEFER_PLACE && p->parse_win == 2048 && p->in.neg_reads == 0 &&
         (p->tally_mode == 1 || (MPC_SUB1 && p->tally_mode == 3 && p->sub_wins == 1))) {
       const int off = (p->parse_lds + 15) & ~15;
-      const int end = off + p->parse_nw * kDefQ * (int)sizeof(uint2);
+      const int end = off + defer_bytes(p->parse_nw, MPC_DEFER_SUBEV && p->tally_mode == 3);
       if (end <= lds_cap && std::max(1, std::min(lds_cap / end, max_waves_cu / p->parse_nw)) == per_cu) {
         p->defer_off = off;
         p->parse_lds = end;

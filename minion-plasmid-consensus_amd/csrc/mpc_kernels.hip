@@ -54,7 +54,7 @@
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
     defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW) || \
-    defined(MPC_PREFETCH_CS_MODES) || defined(MPC_INT_CHECK_MODES) || defined(MPC_DEFER_PLACE) || defined(MPC_DEFER_SUBEV)
+    defined(MPC_PREFETCH_CS_MODES) || defined(MPC_INT_CHECK_MODES) || defined(MPC_DEFER_PLACE) || defined(MPC_DEFER_SUBEV) || defined(MPC_LEFT_INTERP)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -2352,6 +2352,12 @@ __device__ __forceinline__ int64_t run_left(const int32_t* rs, const int32_t* rs
 // buckets become many units) and appends them to one list.
 // ---------------------------------------------------------------------------
 constexpr int kUB = 1024;             // threads of K_ins and of K_left's default geometry
+// K_left: interpolation probes before the binary search of a gap's staged
+// RIGHT reads (ranges over 16); off: bit-exact, C3 +9 us, C4 +13 us, C2 / C5 +-2 us
+// (profiles/r06_experiments/k_left_search_ablations.txt)
+#ifndef MPC_LEFT_INTERP
+#define MPC_LEFT_INTERP 0
+#endif
 constexpr int kLeftVals = 4096;       // mixed RIGHT reads of a bucket staged in K_left's LDS
 constexpr int kEPT = 16;         // events per thread per unit (loads batched)
 constexpr int kUnit = kUB * kEPT;     // events per work unit (K_left<kUB>; K_left<512>: half)
@@ -2641,6 +2647,30 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
         if (vl) {  // 32-bit search of the staged RIGHT reads
           int lo = la - v0, hi = lb - v0;
           const int l0 = lo;
+          if (MPC_LEFT_INTERP && hi - lo > 16) {
+            // interpolation probes first (a gap's RIGHT reads are spread over
+            // the batch's read indices): the range's end values, then up to two
+            // probes at the interpolated index; [lo, hi) keeps
+            // s_vals[< lo] < rg <= s_vals[>= hi], so any probe is exact
+            int32_t vL = s_vals[lo], vH = s_vals[hi - 1];
+            if (rg <= vL) {
+              hi = lo;
+            } else if (rg > vH) {
+              lo = hi;
+            } else {  // vL < rg <= vH
+              int aL = lo, aH = hi - 1;
+              lo = aL + 1;
+              hi = aH;
+#pragma unroll
+              for (int it = 0; it < 2; ++it) {
+                if (hi - lo <= 8) break;
+                const float f = __fdividef((float)(rg - vL), (float)(vH - vL));
+                const int g = min(max(aL + (int)(f * (float)(aH - aL)), lo), hi - 1);
+                const int32_t vg = s_vals[g];
+                if (vg < rg) { aL = g; vL = vg; lo = g + 1; } else { aH = g; vH = vg; hi = g; }
+              }
+            }
+          }
           while (lo < hi) {
             const int mid = (lo + hi) >> 1;
             if (s_vals[mid] < rg) lo = mid + 1; else hi = mid;

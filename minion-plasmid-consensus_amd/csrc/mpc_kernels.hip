@@ -2358,6 +2358,7 @@ constexpr int kUB = 1024;             // threads of K_ins and of K_left's defaul
 #ifndef MPC_LEFT_INTERP
 #define MPC_LEFT_INTERP 0
 #endif
+
 constexpr int kLeftVals = 4096;       // mixed RIGHT reads of a bucket staged in K_left's LDS
 constexpr int kEPT = 16;         // events per thread per unit (loads batched)
 constexpr int kUnit = kUB * kEPT;     // events per work unit (K_left<kUB>; K_left<512>: half)
@@ -2530,6 +2531,9 @@ struct LeftArgs {
 // UB = 1024 at most 64 VGPRs, two 16-wave blocks (LDS ~57 KB each; C3 K_left
 // 312 -> 227 us, C4 387 -> 286 us; 5 VGPRs spill); UB = 512 at most 80 VGPRs
 // and a smaller RIGHT-read stage, three 8-wave blocks (C5 285 -> 218 us)
+#ifdef MPC_LEFT_DIAG  // diagnostic builds only: K_left event paths (mpc_diag_left)
+__device__ unsigned long long g_left_diag[8];
+#endif
 template <int UB>  // threads per block; work units of UB * kEPT events
 __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ? 8 : 6))) void K_left(LeftArgs a) {
   __shared__ int64_t s_key;
@@ -2639,9 +2643,9 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       const int32_t rg = (int32_t)a.read_offset + r0q[q] + (int32_t)(ev >> 16);  // global reads < 2^30
       const int L = (int)((ev >> 8) & 3u) + 1;
       const int p = gap - g0;
-      const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
       // run of the event within its gap: this shard's runs of the gap start at
       // roff (the RIGHT events of lower shards); k counts from there
+      const int32_t la = s_rsl[p], lb = s_rsl[p + 1];
       int32_t k = 0;
       if (lb > la) {
         if (vl) {  // 32-bit search of the staged RIGHT reads
@@ -2684,6 +2688,15 @@ __global__ __launch_bounds__(UB) __attribute__((amdgpu_waves_per_eu(UB == 1024 ?
       // run's slot hi_run - 1 - bi, :37-62): K_ins maps them to rows after the layout
       // LDS slots: the shard's runs of the gap (as many as on one GPU); the
       // global run is s_rs[p] + g + roff + k
+#ifdef MPC_LEFT_DIAG
+      {  // [0] events [1] searched (mixed gap) [2] run k >= kKMax [3] sum of searched ranges [4] k >= 16 [5] k >= 32
+        atomicAdd(&g_left_diag[0], 1ull);
+        if (lb > la) { atomicAdd(&g_left_diag[1], 1ull); atomicAdd(&g_left_diag[3], (unsigned long long)(lb - la)); }
+        if (k >= kKMax) atomicAdd(&g_left_diag[2], 1ull);
+        if (k >= 16) atomicAdd(&g_left_diag[4], 1ull);
+        if (k >= 32) atomicAdd(&g_left_diag[5], 1ull);
+      }
+#endif
       if (k < kKMax) {
         // the run's longest LEFT string: UB = 1024 takes it from the highest
         // slot holding a base at the flush (one LDS atomic less per event: C4
@@ -4037,6 +4050,16 @@ static inline unsigned nblk(int64_t n, int b = 256) {
 extern "C" {
 
 int mpc_version(void) { return MPC_ABI_VERSION; }
+#ifdef MPC_LEFT_DIAG
+int mpc_diag_left(unsigned long long* out, int reset) {
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_left_diag), sizeof(g_left_diag)) != hipSuccess) return -1;
+  if (reset) {
+    static const unsigned long long z[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    if (hipMemcpyToSymbol(HIP_SYMBOL(g_left_diag), z, sizeof(z)) != hipSuccess) return -1;
+  }
+  return 0;
+}
+#endif
 
 int mpc_build_flags(void) { return MPC_BF_STAMPS_ | MPC_BF_TUNING_ | MPC_BF_VARIANT_; }
 

@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MPC_ABI_VERSION 8
+#define MPC_ABI_VERSION 9  /* 9: mpc_plan_info.deferred_placement (struct grew) */
 
 /* return codes */
 #define MPC_OK 0

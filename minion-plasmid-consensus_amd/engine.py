@@ -15,7 +15,7 @@ from . import _build
 
 LIB_PATH = _build.LIBMPC
 
-ABI_VERSION = 8
+ABI_VERSION = 9
 MPC_ST_FLAGS, MPC_ST_FIRST_READ, MPC_ST_ROWS_NEEDED, MPC_ST_MIXED, MPC_ST_RSORT_PATH = 0, 1, 2, 3, 5
 MPC_ST_WRAP_EVENTS, MPC_ST_WRAP_POS = 6, 7
 DE_OP, DE_VALUE, DE_INDEX, DE_KEY, DE_CAPACITY, DE_INTERNAL, DE_UNSUPPORTED = 1, 2, 4, 8, 16, 32, 64

@@ -30,7 +30,7 @@ def test_library_exports_all(pkg):
     for name in declared():
         assert hasattr(lib, name), name
     lib.mpc_version.restype = ctypes.c_int
-    assert lib.mpc_version() == pkg.engine.ABI_VERSION == 8
+    assert lib.mpc_version() == pkg.engine.ABI_VERSION == 9
 
 
 def test_no_oracle_in_product():

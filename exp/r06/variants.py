@@ -51,6 +51,7 @@ VARIANTS = {
                      "          if (j < L && ev == 0x7fffffffu) atomicAdd(tp + 4 * (L - 1 - j) + (int)((ev >> (2 * j)) & 3u), 1u);")],
     "interp": [("#define MPC_LEFT_INTERP 0", "#define MPC_LEFT_INTERP 1")],
     "leftdiag": [("#ifdef MPC_LEFT_DIAG  // diagnostic builds only", "#define MPC_LEFT_DIAG\n#ifdef MPC_LEFT_DIAG  // diagnostic builds only")],
+    "flushx2": [("#define MPC_FLUSH_X2 0", "#define MPC_FLUSH_X2 1")],
     "nodefer": [("#define MPC_DEFER_PLACE 1", "#define MPC_DEFER_PLACE 0")],
     "prefetch": [("#define MPC_PREFETCH_CS_MODES 0x00", "#define MPC_PREFETCH_CS_MODES 0x1f")],
     # both, in tally modes 1 and 2 only (short references: C1, C2)

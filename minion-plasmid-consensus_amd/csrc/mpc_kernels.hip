@@ -54,7 +54,7 @@
 #if defined(MPC_PARSE_DMA) || defined(MPC_FAST_DECODE_MODES) || defined(MPC_LDS_BASE_MODES) || defined(MPC_EPI_U) || \
     defined(MPC_SUBS_SLAB) || defined(MPC_LAYOUT_GAPS) || defined(MPC_LOOKBACK_U) ||     \
     defined(MPC_FLANK_BLOCKS_MAX) || defined(MPC_BPERM_BASE_MODES) || defined(MPC_FLANK_WAVES) || defined(MPC_CS_NT) || defined(MPC_SUB1) || defined(MPC_EARLY_PLACE) || defined(MPC_FLANK_SMALL_BELOW) || \
-    defined(MPC_PREFETCH_CS_MODES) || defined(MPC_INT_CHECK_MODES) || defined(MPC_DEFER_PLACE) || defined(MPC_DEFER_SUBEV) || defined(MPC_LEFT_INTERP)
+    defined(MPC_PREFETCH_CS_MODES) || defined(MPC_INT_CHECK_MODES) || defined(MPC_DEFER_PLACE) || defined(MPC_DEFER_SUBEV) || defined(MPC_LEFT_INTERP) || defined(MPC_FLUSH_X2)
 #define MPC_BF_VARIANT_ 4
 #else
 #define MPC_BF_VARIANT_ 0
@@ -410,6 +410,12 @@ template <int TM> constexpr bool int_check() { return (MPC_INT_CHECK_MODES >> TM
 #define MPC_DEFER_PLACE 1
 #endif
 constexpr int kDefQ = 128;  // queue entries per wave (a power of 2, >= 127)
+// ... and the epilogue flushes the LDS substitution tallies (tally modes 1, 2)
+// with one 64-bit atomic per two codes of a position (off: bit-exact, C1 +6 %,
+// C2 +-0; profiles/r06_experiments/kparse_flush_x2.txt)
+#ifndef MPC_FLUSH_X2
+#define MPC_FLUSH_X2 0
+#endif
 // ... and (tally mode 3 with one substitution window) the 2-byte substitution
 // events too: a ring of kSubQ per wave, written out 128 at a time (two
 // consecutive events per lane) instead of one global store per round
@@ -865,10 +871,21 @@ __device__ void parse_epilogue(const ParseArgs& a, int n, int gb, int nbk, uint3
       if (dv) atomicAdd(a.diff + gb + p, dv);
     }
     uint32_t* sg = a.sub + (int64_t)gb * 4;
-    for (int k = threadIdx.x; lds_sub && k < 4 * (n + 1); k += blockDim.x) {  // word k = position k/4, code k%4
-      const uint32_t w2 = sub_l[2 * (k >> 2) + ((k >> 1) & 1)];
-      const uint32_t v = (k & 1) ? (w2 >> 16) : (w2 & 0xffffu);
-      if (v) atomicAdd(sg + k, v);
+    if (MPC_FLUSH_X2) {
+      // two codes per 64-bit add (LDS word k = position k/2, codes 2 (k&1) + {0, 1}
+      // = global words 2k, 2k + 1): a position's count of one code never
+      // reaches 2^32, so the low half never carries into the high one
+      for (int k = threadIdx.x; lds_sub && k < 2 * (n + 1); k += blockDim.x) {
+        const uint32_t w2 = sub_l[k];
+        if (w2) atomicAdd(reinterpret_cast<unsigned long long*>(sg) + k,
+                          (unsigned long long)(w2 & 0xffffu) | ((unsigned long long)(w2 >> 16) << 32));
+      }
+    } else {
+      for (int k = threadIdx.x; lds_sub && k < 4 * (n + 1); k += blockDim.x) {  // word k = position k/4, code k%4
+        const uint32_t w2 = sub_l[2 * (k >> 2) + ((k >> 1) & 1)];
+        const uint32_t v = (k & 1) ? (w2 >> 16) : (w2 & 0xffffu);
+        if (v) atomicAdd(sg + k, v);
+      }
     }
   }
   for (int k = threadIdx.x; !big && k < parse_hl_words(n); k += blockDim.x) {

@@ -22,7 +22,12 @@ reps = int(os.environ.get("KEXP_REPS", "10"))
 libs = [os.path.abspath(p) for p in sys.argv[1:]]
 eng.LIB_PATH = libs[0]
 eng.lib()
-samples, _ = bench.shard_samples(pkg, cfg, 0, 1)
+if os.environ.get("KEXP_SYNTH"):  # "n,reads": one synthetic sample of that shape instead of a bench config
+    n_, r_ = (int(x) for x in os.environ["KEXP_SYNTH"].split(","))
+    samples = [pkg.synth.Synth(n=n_, n_reads=r_, profile="default", seed=5, frac_partial=0.1).sample(0)]
+    cfg = "synth%d_%d" % (n_, r_)
+else:
+    samples, _ = bench.shard_samples(pkg, cfg, 0, 1)
 batch = eng.Batch(samples)
 st = torch.cuda.current_stream()
 times = {p: ([], []) for p in libs}
